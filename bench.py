@@ -1,0 +1,236 @@
+#!/usr/bin/env python
+"""North-star benchmark: utterances/s (+ RTF) of the MI355X casr path on synthetic fbank of
+shape (B, T, F) = (256, 800, 80) per GPU, greedy decode (headline) and beam = 8 (B = 128).
+
+One step = features (delta/stack/CMVN) -> 4-layer BiLSTM encoder -> attention keys ->
+40-step decode loop -> token ids copied to the host, for one batch per GPU.  Inputs are
+resident in HBM before the timed region.  Multi-GPU: one process per GPU (torchrun), rank 0
+packs the weights and RCCL-broadcasts the packed blob over xGMI; utterance batches are
+independent (no collective in the timed region except the start/stop barriers).
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "chinese-asr_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "utterances/sec + real-time factor, (B,T,F)=(256,800,80) greedy & beam=8"
+PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+AUDIO_S_PER_UTT = 8.0       # 800 frames x 10 ms
+
+
+def fbank_batch(first, B, T, F=80):
+    return np.stack([np.random.RandomState(1234 + first + b).standard_normal((T, F)).astype(np.float32)
+                     for b in range(B)])
+
+
+def kernel_work(cls, B, Tp, R, V, T):
+    """Algorithmic work of ONE step's launches of a kernel class: (flops or bytes, bound)."""
+    H, C, HD, E, A, D = 256, 512, 512, 256, 128, 720
+    if cls == "input_proj":
+        return 2.0 * B * Tp * 8 * H * (D + 3 * C), "mfma"
+    if cls == "rec_step":
+        return 4 * 2.0 * B * Tp * 2 * 4 * H * H, "mfma"
+    if cls == "keys":
+        return 2.0 * B * Tp * A * C, "mfma"
+    if cls == "dec_lstm":
+        return 40 * 2.0 * R * 4 * HD * (E + C + HD), "mfma"
+    if cls == "proj":
+        return 40 * 2.0 * R * V * (C + HD), "mfma"
+    if cls == "attention":   # keys + values streamed once per utterance per step
+        return 40 * 4.0 * B * Tp * (A + C), "hbm"
+    if cls == "select":
+        return 40 * 4.0 * R * V, "hbm"
+    if cls == "features":    # fbank read + stacked rows written, then re-read/written by CMVN
+        return 4.0 * B * (T * 80 + 3 * Tp * D), "hbm"
+    return 0.0, "hbm"
+
+
+def cpu_baseline(n_utt, T):
+    """The CPU oracle (numpy restatement of the reference path, oracle/casr_oracle.py) timed
+    on this host on a bounded sample of the same workload."""
+    sys.path.insert(0, REPO)
+    from oracle import casr_oracle as O
+    from casr.config import CasrConfig
+    from casr.weights import synthetic_state_dicts
+    enc_sd, dec_sd = synthetic_state_dicts(CasrConfig(), peaked=True, eos_bias=0.0)
+    fb = fbank_batch(0, n_utt, T)
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
+    except Exception:
+        cores = os.cpu_count()
+    t0 = time.perf_counter()
+    feats = [O.features_from_fbank(fb[b]) for b in range(n_utt)]
+    O.greedy_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd)
+    dt = time.perf_counter() - t0
+    return {"value": n_utt / dt, "unit": "utt/s", "cores": int(cores), "kind": "port",
+            "sample": f"greedy, {n_utt} utterances x T={T} (all 40 steps), numpy fp32 oracle, {dt:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--frames", type=int, default=800)
+    ap.add_argument("--beam", type=int, default=8)
+    ap.add_argument("--beam-batch", type=int, default=128)
+    ap.add_argument("--beam-steps", type=int, default=2)
+    ap.add_argument("--no-beam", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=48)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from casr.config import CasrConfig
+    from casr.engine import Engine
+    from casr.lib import pack_weights, load as load_lib
+    from casr.weights import synthetic_state_dicts
+
+    cfg = CasrConfig()
+    load_lib()
+    # ---- weights: pack on rank 0, RCCL broadcast of the packed blob
+    t_w = time.perf_counter()
+    if rank == 0:
+        packed = torch.from_numpy(pack_weights(cfg, *synthetic_state_dicts(cfg, peaked=True, eos_bias=0.0))).to(dev)
+        n = torch.tensor([packed.numel()], device=dev)
+    else:
+        n = torch.zeros(1, dtype=torch.int64, device=dev)
+    if dist is not None:
+        dist.broadcast(n, 0)
+        if rank != 0:
+            packed = torch.empty(int(n.item()), dtype=torch.float32, device=dev)
+        dist.broadcast(packed, 0)
+    torch.cuda.synchronize()
+    weight_s = time.perf_counter() - t_w
+    eng = Engine(cfg, packed=packed, device=dev)
+
+    B, T = args.batch, args.frames
+    fb = torch.from_numpy(fbank_batch(rank * B, B, T)).to(dev)
+    frames = torch.full((B,), T, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def step_greedy():
+        feat, flen = eng.features(fb, frames)
+        eng.encode(feat, flen)
+        out = eng.greedy()
+        return out["tokens"].cpu()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def timed(fn, steps):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        barrier()
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if dist is not None:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return float(dt.item())
+
+    for _ in range(args.warmup):
+        step_greedy()
+    # one instrumented step: per-class launch times -> dominant kernel
+    eng.profile(["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"])
+    step_greedy()
+    breakdown = eng.profile_read()
+    dominant = max(breakdown, key=lambda c: breakdown[c][1])
+    # timed region: only the dominant class keeps its event pair per launch
+    eng.profile([dominant])
+    dt = timed(step_greedy, args.steps)
+    dom_launches, dom_ms = eng.profile_read()[dominant]
+    eng.profile([])
+
+    Tp = T // 3
+    value = B * world * args.steps / dt
+    ms_step = 1000.0 * dt / args.steps
+    work, bound = kernel_work(dominant, B, Tp, B, cfg.vocab, T)
+    per_launch_work = work * args.steps / dom_launches
+    avg_launch_s = dom_ms / 1000.0 / dom_launches
+    if bound == "mfma":
+        achieved, peak, unit = per_launch_work / avg_launch_s / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"
+    else:
+        achieved, peak, unit = per_launch_work / avg_launch_s / 1e9, PEAK_HBM_GBS, "GB/s"
+    traffic = None
+    pmc_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_file):
+        try:
+            traffic = json.load(open(pmc_file)).get(dominant)
+        except Exception:
+            traffic = None
+
+    beam = None
+    if not args.no_beam:
+        Bb = args.beam_batch
+        fbb = torch.from_numpy(fbank_batch(rank * Bb, Bb, T)).to(dev)
+        frb = torch.full((Bb,), T, dtype=torch.int32, device=dev)
+
+        def step_beam():
+            feat, flen = eng.features(fbb, frb)
+            eng.encode(feat, flen)
+            r = eng.beam(args.beam)
+            return r["tokens"].cpu()
+
+        step_beam()
+        dtb = timed(step_beam, args.beam_steps)
+        beam = {"k": args.beam, "batch_per_gpu": Bb, "value": Bb * world * args.beam_steps / dtb,
+                "unit": "utt/s", "ms_per_step": 1000.0 * dtb / args.beam_steps,
+                "rtf": dtb / args.beam_steps / (Bb * world * AUDIO_S_PER_UTT)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_sample, T)
+
+    if rank == 0:
+        rec = {
+            "metric": METRIC, "value": value, "unit": "utt/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic fbank RandomState(1234+b) (800x80); deterministic synthetic weights "
+                    "(SURVEY 8d recipe, proj x40, no EOS bias: all 40 decode steps run)",
+            "config": {"workload": f"greedy decode, B={B}/GPU, T={T}, F=80: features + 4-layer BiLSTM "
+                                   f"encoder + 40-step attention decode, ids to host",
+                       "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
+            "rtf": dt / args.steps / (B * world * AUDIO_S_PER_UTT),
+            "beam": beam,
+            "roofline": {"kernel": dominant, "bound": bound, "achieved": achieved, "peak": peak,
+                         "unit": unit, "frac": achieved / peak, "traffic": traffic,
+                         "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s},
+            "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},
+            "weights_bcast_s": weight_s,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            rec["speedup_vs_cpu"] = value / cpu["value"]
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,158 @@
+"""Device-side engine: one casr handle per GPU, torch tensors as caller-owned buffers.
+
+PyTorch supplies device memory, the current HIP stream and (for multi-GPU) RCCL; every
+compute step is a call into the HIP C-ABI library.  There is no CPU or torch-op fallback:
+without a GPU or the library, construction raises.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import lib as _lib
+from .config import CasrConfig
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class Engine:
+    """casr handle bound to packed weights on one device."""
+
+    def __init__(self, cfg: CasrConfig, enc_sd=None, dec_sd=None, device=None, packed=None):
+        if not torch.cuda.is_available():
+            raise _lib.CasrError("casr Engine needs an MI355X GPU (torch.cuda.is_available() is False)")
+        self.cfg = cfg
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
+                                   torch.device(device).index or 0)
+        self.lib = _lib.load()
+        self.handle = ctypes.c_void_p()
+        c = _lib.config_struct(cfg)
+        _lib.check(self.lib.casr_create(ctypes.byref(c), self.device.index, ctypes.byref(self.handle)))
+        if packed is None:
+            packed = _lib.pack_weights(cfg, enc_sd, dec_sd)
+        self.bind(packed)
+        self._B = self._Tp = None
+
+    def bind(self, packed):
+        """packed: host numpy blob or a device tensor (e.g. received by RCCL broadcast)."""
+        if isinstance(packed, np.ndarray):
+            packed = torch.from_numpy(packed).to(self.device)
+        if packed.device != self.device or packed.dtype != torch.float32:
+            raise ValueError("packed weights must be a float32 tensor on the engine device")
+        self.packed = packed.contiguous()
+        _lib.check(self.lib.casr_bind_weights(self.handle, _ptr(self.packed)), self.handle)
+
+    def close(self):
+        if self.handle:
+            self.lib.casr_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ features
+    def features(self, fbank, frames, eps=1e-6):
+        """fbank [B, T, n_mels] float32 (device), frames [B] int32 (device) ->
+        (feat [B, T//3, feat_dim], feat_len [B] int32)."""
+        fbank = fbank.contiguous()
+        B, T, _ = fbank.shape
+        feat = torch.empty(B, T // 3, self.cfg.feat_dim, device=self.device, dtype=torch.float32)
+        flen = torch.empty(B, device=self.device, dtype=torch.int32)
+        _lib.check(self.lib.casr_features(self.handle, _ptr(fbank), _ptr(frames.to(torch.int32).contiguous()),
+                                          B, T, ctypes.c_float(eps), _ptr(feat), _ptr(flen), _stream()),
+                   self.handle)
+        return feat, flen
+
+    def gather(self, utts, lens, Tp=None):
+        """list of B device tensors [T_b, feat_dim] -> padded [B, Tp, feat_dim]."""
+        B = len(utts)
+        utts = [u.contiguous().to(self.device, torch.float32) for u in utts]
+        Tp = int(max(int(u.shape[0]) for u in utts)) if Tp is None else Tp
+        ptrs = torch.tensor([u.data_ptr() for u in utts], dtype=torch.int64, device=self.device)
+        lens_d = lens.to(self.device, torch.int32).contiguous()
+        feat = torch.empty(B, Tp, self.cfg.feat_dim, device=self.device, dtype=torch.float32)
+        _lib.check(self.lib.casr_gather_utterances(self.handle, _ptr(ptrs), _ptr(lens_d), B, Tp, _ptr(feat),
+                                                   _stream()), self.handle)
+        self._keep = (utts, ptrs)
+        return feat, lens_d
+
+    # ------------------------------------------------------------------ encoder
+    def encode(self, feat, lens):
+        feat = feat.contiguous()
+        B, Tp, _ = feat.shape
+        lens = lens.to(self.device, torch.int32).contiguous()
+        _lib.check(self.lib.casr_encode(self.handle, _ptr(feat), _ptr(lens), B, Tp, _stream()), self.handle)
+        self._B, self._Tp = B, Tp
+        self._lens = lens
+
+    def encoder_results(self):
+        B, Tp, Cz = self._B, self._Tp, 2 * self.cfg.enc_hidden
+        enc = torch.empty(B, Tp, Cz, device=self.device)
+        h = torch.empty(B, Cz, device=self.device)
+        c = torch.empty(B, Cz, device=self.device)
+        keys = torch.empty(B, self.cfg.attn_size, Tp, device=self.device)
+        _lib.check(self.lib.casr_encoder_results(self.handle, _ptr(enc), _ptr(h), _ptr(c), _ptr(keys),
+                                                 _stream()), self.handle)
+        return enc, h, c, keys
+
+    # ------------------------------------------------------------------ decode
+    def greedy(self, alignment=False):
+        B, L = self._B, self.cfg.max_len
+        dev = self.device
+        tokens = torch.empty(B, L, dtype=torch.int32, device=dev)
+        out_len = torch.empty(B, dtype=torch.int32, device=dev)
+        fin = torch.empty(B, dtype=torch.uint8, device=dev)
+        accum = torch.empty(B, dtype=torch.float32, device=dev)
+        align = torch.zeros(L, self._Tp, B, device=dev) if alignment else None
+        _lib.check(self.lib.casr_greedy(self.handle, _ptr(tokens), _ptr(out_len), _ptr(fin), _ptr(accum),
+                                        _ptr(align), _stream()), self.handle)
+        return dict(tokens=tokens, out_len=out_len, finished=fin, accum=accum, alignment=align)
+
+    def beam(self, k, lm_weight=0.0, length_weight=0.0):
+        B, L = self._B, self.cfg.max_len
+        dev = self.device
+        toks = torch.empty(B, L, dtype=torch.int32, device=dev)
+        blen = torch.empty(B, dtype=torch.int32, device=dev)
+        score = torch.empty(B, dtype=torch.float32, device=dev)
+        steps = torch.empty(1, dtype=torch.int32, device=dev)
+        _lib.check(self.lib.casr_beam(self.handle, int(k), ctypes.c_float(lm_weight), ctypes.c_float(length_weight),
+                                      _ptr(toks), _ptr(blen), _ptr(score), _ptr(steps), _stream()), self.handle)
+        self._k = k
+        return dict(tokens=toks, length=blen, score=score, steps=steps)
+
+    def beam_records(self):
+        B, L, k = self._B, self.cfg.max_len, self._k
+        dev = self.device
+        rt = torch.empty(B, L, k, L, dtype=torch.int32, device=dev)
+        rs = torch.empty(B, L, k, dtype=torch.float32, device=dev)
+        rv = torch.empty(B, L, k, dtype=torch.uint8, device=dev)
+        _lib.check(self.lib.casr_beam_records(self.handle, _ptr(rt), _ptr(rs), _ptr(rv), _stream()), self.handle)
+        return rt, rs, rv
+
+    # ------------------------------------------------------------------ launch timing
+    def profile(self, classes):
+        """Enable HIP-event timing for the named kernel classes (lib.KERNEL_CLASSES)."""
+        mask = 0
+        for c in classes:
+            mask |= 1 << _lib.KERNEL_CLASSES.index(c)
+        _lib.check(self.lib.casr_profile_enable(self.handle, mask), self.handle)
+
+    def profile_read(self):
+        """{class: (launches, total_ms)} for the enabled classes since profile()."""
+        out = {}
+        for i, name in enumerate(_lib.KERNEL_CLASSES):
+            n = ctypes.c_int32()
+            ms = ctypes.c_double()
+            _lib.check(self.lib.casr_profile_read(self.handle, i, ctypes.byref(n), ctypes.byref(ms)), self.handle)
+            if n.value:
+                out[name] = (n.value, ms.value)
+        return out

@@ -1,0 +1,81 @@
+"""Host-side result assembly with the reference's exact finalize rules.
+
+The device returns integer token arrays and float32 scores; this module turns them into the
+reference's Python results: greedy (model.py:582-602), beam first-max / second-pass
+selection (parse_finished_tensors, model.py:708-765) and the unfinished fallback
+(model.py:961-972).  Also the reference's record types (util.py:2403-2406)."""
+from collections import namedtuple
+
+import numpy as np
+
+EvalOutput = namedtuple('EvalOutput', ('pred_text', 'score', 'text', 'wer', 'n', 'alignment',
+                                       'audio_feat_len', 'text_len'))
+EncoderOutput = namedtuple('EncoderOutput', ('out', 'out_lens', 'state'))
+DecoderOutput = namedtuple('DecoderOutput', ('logit', 'attn_hidden_state', 'alignment', 'cell_state'))
+
+
+def edit_distance(a, b):
+    """Levenshtein distance (the reference calls python-Levenshtein, util.py:237-262)."""
+    m, n = len(a), len(b)
+    if m == 0:
+        return n
+    if n == 0:
+        return m
+    prev = list(range(n + 1))
+    for i in range(1, m + 1):
+        cur = [i] + [0] * n
+        ai = a[i - 1]
+        for j in range(1, n + 1):
+            cur[j] = prev[j - 1] if ai == b[j - 1] else 1 + min(prev[j - 1], prev[j], cur[j - 1])
+        prev = cur
+    return prev[n]
+
+
+def get_wer(pred, ref):
+    """util.py:237-249 with normalize=True: distance / len(ref)."""
+    return edit_distance(pred, ref) / (1.0 * len(ref))
+
+
+def greedy_outputs(tokens, out_len, finished, accum):
+    """model.py:582-593.  Host numpy inputs.  Returns (token lists, scores)."""
+    toks = [tokens[b, :out_len[b]].tolist() for b in range(tokens.shape[0])]
+    score = []
+    for b, t in enumerate(toks):
+        if len(t) == 0:
+            score.append(0.0)
+        else:
+            score.append(float(accum[b]) / (int(out_len[b]) + int(finished[b])))
+    return toks, score
+
+
+def greedy_steps(out_len, finished, max_len):
+    """Iterations the reference loop runs (model.py:578 breaks once all are finished)."""
+    if len(finished) and bool(np.all(finished)):
+        return int(np.max(out_len)) + 1
+    return max_len
+
+
+def records_by_utterance(rec_tokens, rec_score, rec_valid):
+    """Finished hypotheses per utterance in the reference's list order (step, then rank):
+    b -> [(tokens, score)] (model.py:715-733)."""
+    B, L, k = rec_valid.shape
+    res = {}
+    for b, l, c in zip(*np.nonzero(rec_valid)):
+        res.setdefault(int(b), []).append((int(l), int(c), rec_tokens[b, l, c, :l].tolist(),
+                                           float(rec_score[b, l, c])))
+    return {b: [(t, s) for _, _, t, s in sorted(v)] for b, v in res.items()}
+
+
+def second_pass_select(records, int2word, lm_model, lm_weight, length_weight):
+    """parse_finished_tensors with second_pass (model.py:749-763): for > 1 finished
+    hypotheses pick argmax(logp + lm_w * LM(' '.join(words), bos=True) + len_w * len);
+    returns the original (tokens, logp)."""
+    out = {}
+    for b, v in records.items():
+        if len(v) == 1:
+            out[b] = v[0]
+            continue
+        lm = [lm_model.score(' '.join([int2word[i] for i in t]), bos=True) for t, _ in v]
+        comb = [s + lm_weight * q + length_weight * len(t) for (t, s), q in zip(v, lm)]
+        out[b] = v[int(np.argmax(comb))]
+    return out

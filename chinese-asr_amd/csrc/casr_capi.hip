@@ -1,0 +1,471 @@
+// Host side of the casr C ABI (include/casr.h): weight packing into kernel layouts,
+// per-handle device workspaces, and the encode / decode drivers.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "casr.h"
+#include "casr_internal.h"
+
+namespace casr {
+
+size_t attention_smem_bytes(int k, int Tp);  // decoder.hip
+
+Layout make_layout(const casr_config& cfg) {
+  Layout L{};
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    const size_t o = off;
+    off += (n + 63) & ~size_t(63);  // 256 B alignment for every tensor
+    return o;
+  };
+  L.layers = cfg.enc_layers;
+  L.V = cfg.vocab;
+  L.VP = (cfg.vocab + 63) / 64 * 64;
+  for (int l = 0; l < cfg.enc_layers; ++l) {
+    const int din = l == 0 ? D : C;
+    L.enc_wih[l] = take((size_t)8 * H * din);
+    L.enc_bias[l] = take((size_t)8 * H);
+    L.enc_whh[l] = take((size_t)2 * 4 * H * H);
+  }
+  L.emb = take((size_t)cfg.vocab * E);
+  L.dec_w = take((size_t)4 * HD * KDEC);
+  L.dec_b = take((size_t)4 * HD);
+  L.proj_w = take((size_t)L.VP * KPROJ);
+  L.proj_b = take((size_t)L.VP);
+  L.wencT = take((size_t)A * C);
+  L.b_attn = take((size_t)A);
+  L.w_hidden = take((size_t)HD * A);
+  L.v = take((size_t)A);
+  L.total = off;
+  return L;
+}
+
+// Write a [N][K] matrix (element accessor f(n, k), rows >= N zero) in MFMA-fragment-major
+// order: 16-row x 64-k blocks, block (nt, kc) at (nt*NKC + kc)*FRAG, inside [q][lane][4]
+// with lane row = lane&15, k = 16*(lane>>4) + 4q + e.
+template <class Fn>
+static void pack_frag(float* dst, int NT, int NKC, Fn f) {
+  for (int nt = 0; nt < NT; ++nt)
+    for (int kc = 0; kc < NKC; ++kc) {
+      float* blk = dst + ((size_t)nt * NKC + kc) * FRAG;
+      for (int q = 0; q < 4; ++q)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < 4; ++e) {
+            const int n = nt * 16 + (lane & 15);
+            const int k = kc * 64 + 16 * (lane >> 4) + 4 * q + e;
+            blk[(q * 64 + lane) * 4 + e] = f(n, k);
+          }
+    }
+}
+
+}  // namespace casr
+
+using namespace casr;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipSuccess) n = bytes;
+    return e;
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct casr_handle {
+  casr_config cfg{};
+  Layout L{};
+  int device = 0;
+  const float* W = nullptr;
+  std::string err;
+  // encoder workspace
+  DevBuf gin, out0, out1, hbuf, cst, hfin, keysT, lens;
+  int B = 0, Tp = 0;
+  bool encoded = false;
+  float* enc_out = nullptr;  // out0 or out1
+  // decoder workspace
+  DevBuf st, logits, small, bp, tk, rec, beam_small;
+  DecodeBufs d{};
+  Profiler prof;
+  int dec_k = 0;
+  bool beam_done = false;
+};
+
+static int fail(casr_handle* h, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (h) h->err = buf;
+  g_err = buf;
+  return code;
+}
+
+#define HIP_OK(h, expr)                                                                \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail((h), CASR_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                  __FILE__, __LINE__);                                                 \
+  } while (0)
+
+static int check_config(const casr_config* c) {
+  if (!c) return fail(nullptr, CASR_ERR_ARG, "config is NULL");
+  if (c->n_mels != F || c->feat_dim != D || c->enc_hidden != H || c->dec_hidden != HD ||
+      c->embed_dim != E || c->attn_size != A)
+    return fail(nullptr, CASR_ERR_UNSUPPORTED,
+                "this build implements n_mels=80 feat_dim=720 enc_hidden=256 dec_hidden=512 "
+                "embed_dim=256 attn_size=128 (got %d %d %d %d %d %d)",
+                c->n_mels, c->feat_dim, c->enc_hidden, c->dec_hidden, c->embed_dim, c->attn_size);
+  if (c->enc_layers < 1 || c->enc_layers > CASR_MAX_LAYERS || c->vocab < 4 || c->max_len < 1 ||
+      c->sos < 0 || c->sos >= c->vocab || c->eos < 0 || c->eos >= c->vocab || !(c->temperature > 0.f))
+    return fail(nullptr, CASR_ERR_ARG, "invalid config (layers=%d vocab=%d max_len=%d)",
+                c->enc_layers, c->vocab, c->max_len);
+  return CASR_OK;
+}
+
+extern "C" {
+
+int casr_api_version(void) { return CASR_API_VERSION; }
+
+size_t casr_packed_weights_floats(const casr_config* cfg) {
+  if (check_config(cfg) != CASR_OK) return 0;
+  return make_layout(*cfg).total;
+}
+
+int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float* out) {
+  int rc = check_config(cfg);
+  if (rc) return rc;
+  if (!w || !out) return fail(nullptr, CASR_ERR_ARG, "weights/out is NULL");
+  const Layout L = make_layout(*cfg);
+  std::memset(out, 0, L.total * sizeof(float));
+  const int V = cfg->vocab;
+  for (int l = 0; l < cfg->enc_layers; ++l) {
+    const int din = l == 0 ? D : C;
+    for (int d = 0; d < 2; ++d)
+      if (!w->enc_w_ih[l][d] || !w->enc_w_hh[l][d] || !w->enc_b_ih[l][d] || !w->enc_b_hh[l][d])
+        return fail(nullptr, CASR_ERR_ARG, "encoder layer %d dir %d: NULL tensor", l, d);
+    // input projection rows: d*4H + packed(g, u) <- W_ih_d[g*H + u]
+    for (int d = 0; d < 2; ++d)
+      for (int g = 0; g < 4; ++g)
+        for (int u = 0; u < H; ++u) {
+          const int pr = d * 4 * H + packed_gate_row(g, u);
+          const int orow = g * H + u;
+          std::memcpy(out + L.enc_wih[l] + (size_t)pr * din, w->enc_w_ih[l][d] + (size_t)orow * din,
+                      sizeof(float) * din);
+          out[L.enc_bias[l] + pr] = w->enc_b_ih[l][d][orow] + w->enc_b_hh[l][d][orow];
+        }
+    // recurrent matrices, fragment-major per direction: n-tile (jb*4 + g) = gate g of units
+    // jb*16 .. jb*16+15
+    for (int d = 0; d < 2; ++d) {
+      const float* Whh = w->enc_w_hh[l][d];
+      pack_frag(out + L.enc_whh[l] + (size_t)d * 4 * H * H, 4 * H / 16, H / 64, [&](int n, int k) {
+        const int jb = n / 64, g = (n / 16) % 4, u = jb * 16 + (n % 16);
+        return Whh[(size_t)(g * H + u) * H + k];
+      });
+    }
+  }
+  if (!w->embedding || !w->dec_w_ih || !w->dec_w_hh || !w->dec_b_ih || !w->dec_b_hh || !w->proj_w ||
+      !w->proj_b || !w->attn_w_enc || !w->attn_b || !w->attn_w_hidden || !w->attn_v)
+    return fail(nullptr, CASR_ERR_ARG, "decoder/attention: NULL tensor");
+  std::memcpy(out + L.emb, w->embedding, sizeof(float) * (size_t)V * E);
+  // decoder LSTM: K order [emb | ctx | h] = [W_ih | W_hh]
+  pack_frag(out + L.dec_w, 4 * HD / 16, KDEC / 64, [&](int n, int k) {
+    const int jb = n / 64, g = (n / 16) % 4, u = jb * 16 + (n % 16);
+    const int orow = g * HD + u;
+    return k < E + C ? w->dec_w_ih[(size_t)orow * (E + C) + k] : w->dec_w_hh[(size_t)orow * HD + (k - E - C)];
+  });
+  for (int g = 0; g < 4; ++g)
+    for (int u = 0; u < HD; ++u)
+      out[L.dec_b + packed_gate_row(g, u)] = w->dec_b_ih[g * HD + u] + w->dec_b_hh[g * HD + u];
+  // projection: reference input is cat([h, ctx]) (decoder.py:131); packed K order [ctx | h]
+  pack_frag(out + L.proj_w, L.VP / 16, KPROJ / 64, [&](int n, int k) {
+    if (n >= V) return 0.f;
+    return k < C ? w->proj_w[(size_t)n * KPROJ + HD + k] : w->proj_w[(size_t)n * KPROJ + (k - C)];
+  });
+  for (int n = 0; n < V; ++n) out[L.proj_b + n] = w->proj_b[n];
+  for (int a = 0; a < A; ++a)
+    for (int c = 0; c < C; ++c) out[L.wencT + (size_t)a * C + c] = w->attn_w_enc[(size_t)c * A + a];
+  std::memcpy(out + L.b_attn, w->attn_b, sizeof(float) * A);
+  std::memcpy(out + L.w_hidden, w->attn_w_hidden, sizeof(float) * HD * A);
+  std::memcpy(out + L.v, w->attn_v, sizeof(float) * A);
+  return CASR_OK;
+}
+
+int casr_create(const casr_config* cfg, int device, casr_handle** out) {
+  if (!out) return fail(nullptr, CASR_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  int rc = check_config(cfg);
+  if (rc) return rc;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(nullptr, CASR_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= n) return fail(nullptr, CASR_ERR_ARG, "device %d out of range", device);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(nullptr, CASR_ERR_UNSUPPORTED, "device %d is %s; this library is built for gfx950",
+                device, prop.gcnArchName);
+  auto* h = new casr_handle();
+  h->cfg = *cfg;
+  h->L = make_layout(*cfg);
+  h->device = device;
+  *out = h;
+  return CASR_OK;
+}
+
+int casr_bind_weights(casr_handle* h, const float* packed_device) {
+  if (!h || !packed_device) return fail(h, CASR_ERR_ARG, "handle/weights NULL");
+  h->W = packed_device;
+  return CASR_OK;
+}
+
+void casr_destroy(casr_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens,
+                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small})
+    b->release();
+  delete h;
+}
+
+const char* casr_last_error(const casr_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int casr_features(casr_handle* h, const float* fbank, const int32_t* frames, int B, int T, float eps,
+                  float* feat, int32_t* feat_len, void* stream) {
+  if (!h || !fbank || !frames || !feat || !feat_len || B <= 0 || T < 3)
+    return fail(h, CASR_ERR_ARG, "casr_features: bad arguments (B=%d T=%d)", B, T);
+  HIP_OK(h, hipSetDevice(h->device));
+  ProfScope ps(&h->prof, CASR_K_FEATURES, (hipStream_t)stream);
+  HIP_OK(h, launch_features(fbank, frames, B, T, eps, feat, feat_len, (hipStream_t)stream));
+  return CASR_OK;
+}
+
+int casr_gather_utterances(casr_handle* h, const float* const* utt_ptrs, const int32_t* lens, int B,
+                           int Tp, float* feat, void* stream) {
+  if (!h || !utt_ptrs || !lens || !feat || B <= 0 || Tp <= 0)
+    return fail(h, CASR_ERR_ARG, "casr_gather_utterances: bad arguments");
+  HIP_OK(h, hipSetDevice(h->device));
+  HIP_OK(h, launch_gather_utts(utt_ptrs, lens, B, Tp, feat, (hipStream_t)stream));
+  return CASR_OK;
+}
+
+int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, int Tp, void* stream) {
+  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
+  if (!h->W) return fail(h, CASR_ERR_STATE, "casr_encode: no weights bound");
+  if (!feat || !lens || B <= 0 || Tp <= 0) return fail(h, CASR_ERR_ARG, "casr_encode: bad arguments");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  const size_t rows = (size_t)B * Tp;
+  HIP_OK(h, h->gin.ensure(rows * 8 * H * sizeof(float)));
+  HIP_OK(h, h->out0.ensure(rows * C * sizeof(float)));
+  HIP_OK(h, h->out1.ensure(rows * C * sizeof(float)));
+  HIP_OK(h, h->hbuf.ensure((size_t)2 * 2 * B * H * sizeof(float)));
+  HIP_OK(h, h->cst.ensure((size_t)2 * B * H * sizeof(float)));
+  HIP_OK(h, h->hfin.ensure((size_t)2 * B * H * sizeof(float)));
+  HIP_OK(h, h->keysT.ensure(rows * A * sizeof(float)));
+  HIP_OK(h, h->lens.ensure((size_t)B * sizeof(int32_t)));
+  HIP_OK(h, hipMemcpyAsync(h->lens.p, lens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  HIP_OK(h, hipMemsetAsync(h->out0.p, 0, rows * C * sizeof(float), s));
+  HIP_OK(h, hipMemsetAsync(h->out1.p, 0, rows * C * sizeof(float), s));
+  HIP_OK(h, hipMemsetAsync(h->hfin.p, 0, (size_t)2 * B * H * sizeof(float), s));
+  const int32_t* dl = h->lens.as<int32_t>();
+  float* outs[2] = {h->out0.as<float>(), h->out1.as<float>()};
+  const float* x = feat;
+  float* hb = h->hbuf.as<float>();
+  for (int l = 0; l < h->cfg.enc_layers; ++l) {
+    const int din = l == 0 ? D : C;
+    float* out = outs[l & 1];
+    {
+    ProfScope ps(&h->prof, CASR_K_INPUT_PROJ, s);
+    HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
+                                h->gin.as<float>(), s));
+    }
+    HIP_OK(h, hipMemsetAsync(hb, 0, (size_t)2 * B * H * sizeof(float), s));
+    HIP_OK(h, hipMemsetAsync(h->cst.p, 0, (size_t)2 * B * H * sizeof(float), s));
+    const int residual = (h->cfg.residual && l > 0) ? 1 : 0;
+    for (int step = 0; step < Tp; ++step) {
+      const float* hprev = hb + (size_t)(step & 1) * 2 * B * H;
+      float* hnext = hb + (size_t)((step + 1) & 1) * 2 * B * H;
+      ProfScope ps(&h->prof, CASR_K_REC_STEP, s);
+      HIP_OK(h, launch_rec_step(h->W + h->L.enc_whh[l], h->gin.as<float>(), x, out, hprev, hnext,
+                                h->cst.as<float>(), h->hfin.as<float>(), dl, B, Tp, step, residual, s));
+    }
+    x = out;
+  }
+  h->enc_out = const_cast<float*>(x);
+  {
+  ProfScope ps(&h->prof, CASR_K_KEYS, s);
+  HIP_OK(h, launch_keys(h->enc_out, B, Tp, h->W + h->L.wencT, h->W + h->L.b_attn, h->keysT.as<float>(), s));
+  }
+  h->B = B;
+  h->Tp = Tp;
+  h->encoded = true;
+  h->beam_done = false;
+  return CASR_OK;
+}
+
+int casr_encoder_results(casr_handle* h, float* enc, float* h_final, float* c_final, float* keys,
+                         void* stream) {
+  if (!h || !h->encoded) return fail(h, CASR_ERR_STATE, "casr_encoder_results: nothing encoded");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int B = h->B, Tp = h->Tp;
+  if (enc)
+    HIP_OK(h, hipMemcpyAsync(enc, h->enc_out, (size_t)B * Tp * C * sizeof(float), hipMemcpyDeviceToDevice, s));
+  // [2][B][H] -> [B][fw | bw]
+  if (h_final)
+    HIP_OK(h, hipMemcpy2DAsync(h_final, C * sizeof(float), h->hfin.p, H * sizeof(float), H * sizeof(float), B,
+                               hipMemcpyDeviceToDevice, s));
+  if (h_final)
+    HIP_OK(h, hipMemcpy2DAsync(h_final + H, C * sizeof(float), h->hfin.as<float>() + (size_t)B * H,
+                               H * sizeof(float), H * sizeof(float), B, hipMemcpyDeviceToDevice, s));
+  if (c_final)
+    HIP_OK(h, hipMemcpy2DAsync(c_final, C * sizeof(float), h->cst.p, H * sizeof(float), H * sizeof(float), B,
+                               hipMemcpyDeviceToDevice, s));
+  if (c_final)
+    HIP_OK(h, hipMemcpy2DAsync(c_final + H, C * sizeof(float), h->cst.as<float>() + (size_t)B * H,
+                               H * sizeof(float), H * sizeof(float), B, hipMemcpyDeviceToDevice, s));
+  if (keys)
+    HIP_OK(h, hipMemcpyAsync(keys, h->keysT.p, (size_t)B * Tp * A * sizeof(float), hipMemcpyDeviceToDevice, s));
+  return CASR_OK;
+}
+
+static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
+  if (!h->encoded) return fail(h, CASR_ERR_STATE, "decode before casr_encode");
+  if (k < 1 || k > KMAX_BEAM) return fail(h, CASR_ERR_ARG, "beam width %d not in [1, %d]", k, KMAX_BEAM);
+  const int B = h->B, Tp = h->Tp, L = h->cfg.max_len, V = h->cfg.vocab;
+  const int R = B * k;
+  const size_t smem = attention_smem_bytes(k, Tp);
+  if (smem > 160 * 1024)
+    return fail(h, CASR_ERR_UNSUPPORTED, "attention needs %zu B of LDS (k=%d, Tp=%d) > 160 KiB", smem, k, Tp);
+  HIP_OK(h, h->st.ensure((size_t)2 * R * ST * sizeof(float)));
+  HIP_OK(h, h->logits.ensure((size_t)R * V * sizeof(float)));
+  HIP_OK(h, h->small.ensure((size_t)(6 * R + L + B + R) * sizeof(int32_t) + 256));
+  HIP_OK(h, h->bp.ensure((size_t)L * R * sizeof(int32_t)));
+  HIP_OK(h, h->tk.ensure((size_t)L * R * sizeof(int32_t)));
+  HIP_OK(h, h->rec.ensure((size_t)B * L * k * (sizeof(float) + sizeof(int32_t) + 1) + 256));
+  DecodeBufs& d = h->d;
+  d.st[0] = h->st.as<float>();
+  d.st[1] = d.st[0] + (size_t)R * ST;
+  d.logits = h->logits.as<float>();
+  int32_t* sp = h->small.as<int32_t>();
+  d.tok[0] = sp;
+  d.tok[1] = sp + R;
+  d.src[0] = sp + 2 * R;
+  d.src[1] = sp + 3 * R;
+  d.score[0] = reinterpret_cast<float*>(sp + 4 * R);
+  d.score[1] = reinterpret_cast<float*>(sp + 5 * R);
+  d.newdone = sp + 6 * R;
+  d.topfin = reinterpret_cast<uint8_t*>(sp + 6 * R + L);
+  d.fin = reinterpret_cast<uint8_t*>(sp + 6 * R + L + B);
+  d.bp = h->bp.as<int32_t>();
+  d.tk = h->tk.as<int32_t>();
+  d.rec_score = h->rec.as<float>();
+  d.rec_src = reinterpret_cast<int32_t*>(d.rec_score + (size_t)B * L * k);
+  d.rec_valid = reinterpret_cast<uint8_t*>(d.rec_src + (size_t)B * L * k);
+  a.W = h->W;
+  a.L = h->L;
+  a.enc = h->enc_out;
+  a.keysT = h->keysT.as<float>();
+  a.hfin = h->hfin.as<float>();
+  a.cfin = h->cst.as<float>();
+  a.lens = h->lens.as<int32_t>();
+  a.B = B;
+  a.Tp = Tp;
+  a.k = k;
+  a.V = V;
+  a.max_len = L;
+  a.sos = h->cfg.sos;
+  a.eos = h->cfg.eos;
+  a.temperature = h->cfg.temperature;
+  a.prof = &h->prof;
+  return CASR_OK;
+}
+
+int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* finished, float* accum,
+                float* align, void* stream) {
+  if (!h || !tokens || !out_len || !finished || !accum) return fail(h, CASR_ERR_ARG, "casr_greedy: NULL output");
+  HIP_OK(h, hipSetDevice(h->device));
+  DecodeArgs a{};
+  int rc = prepare_decode(h, 1, a);
+  if (rc) return rc;
+  HIP_OK(h, run_greedy(a, h->d, tokens, out_len, finished, accum, align, (hipStream_t)stream));
+  return CASR_OK;
+}
+
+int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32_t* best_tokens,
+              int32_t* best_len, float* best_score, int32_t* steps, void* stream) {
+  if (!h || !best_tokens || !best_len || !best_score || !steps)
+    return fail(h, CASR_ERR_ARG, "casr_beam: NULL output");
+  HIP_OK(h, hipSetDevice(h->device));
+  DecodeArgs a{};
+  int rc = prepare_decode(h, k, a);
+  if (rc) return rc;
+  HIP_OK(h, run_beam(a, h->d, lm_weight, length_weight, best_tokens, best_len, best_score, steps,
+                     (hipStream_t)stream));
+  h->dec_k = k;
+  h->beam_done = true;
+  return CASR_OK;
+}
+
+int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uint8_t* rec_valid,
+                      void* stream) {
+  if (!h || !h->beam_done) return fail(h, CASR_ERR_STATE, "casr_beam_records before casr_beam");
+  if (!rec_tokens || !rec_score || !rec_valid) return fail(h, CASR_ERR_ARG, "casr_beam_records: NULL output");
+  HIP_OK(h, hipSetDevice(h->device));
+  DecodeArgs a{};
+  int rc = prepare_decode(h, h->dec_k, a);
+  if (rc) return rc;
+  HIP_OK(h, run_beam_records(a, h->d, rec_tokens, rec_score, rec_valid, (hipStream_t)stream));
+  return CASR_OK;
+}
+
+int casr_profile_enable(casr_handle* h, uint32_t class_mask) {
+  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
+  h->prof.mask = class_mask;
+  h->prof.reset();
+  return CASR_OK;
+}
+
+int casr_profile_read(casr_handle* h, int cls, int32_t* launches, double* total_ms) {
+  if (!h || cls < 0 || cls >= CASR_K_COUNT || !launches || !total_ms)
+    return fail(h, CASR_ERR_ARG, "casr_profile_read: bad arguments");
+  Profiler& p = h->prof;
+  const size_t n = p.used[cls] / 2;
+  double ms = 0.0;
+  if (n) HIP_OK(h, hipEventSynchronize(p.ev[cls][2 * n - 1]));
+  for (size_t i = 0; i < n; ++i) {
+    float t = 0.f;
+    HIP_OK(h, hipEventElapsedTime(&t, p.ev[cls][2 * i], p.ev[cls][2 * i + 1]));
+    ms += t;
+  }
+  *launches = (int32_t)n;
+  *total_ms = ms;
+  return CASR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,148 @@
+// Internal contracts between the casr host code (casr_capi.hip) and the kernel TUs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "casr.h"
+
+namespace casr {
+
+// Dimensions of the deployed configuration (gpd.py), fixed at compile time so every
+// tile loop unrolls.  casr_create rejects any other configuration (CASR_ERR_UNSUPPORTED).
+constexpr int F = 80;     // n_mels
+constexpr int D = 720;    // encoder input (3 ch x 3 frames x 80)
+constexpr int H = 256;    // encoder hidden per direction
+constexpr int C = 512;    // encoder output / context size (2H)
+constexpr int HD = 512;   // decoder hidden
+constexpr int E = 256;    // embedding
+constexpr int A = 128;    // attention size
+constexpr int KDEC = E + C + HD;  // 1280: decoder LSTM contraction [emb | ctx | h]
+constexpr int KPROJ = C + HD;     // 1024: projection contraction [ctx | h]
+constexpr int ST = C + HD + HD;   // 1536: per-row decoder state [ctx | h | c]
+constexpr int KMAX_BEAM = 16;
+
+// MFMA-fragment-major weight block: a 16-row x 64-k tile stored as [q=0..3][lane][4] so
+// lane l reads row (l&15), k = 16*(l>>4) + 4q + e with one coalesced 16 B load per q.
+constexpr int FRAG = 16 * 64;
+
+// Offsets (in floats) of every tensor inside the packed weight blob.
+struct Layout {
+  size_t enc_wih[CASR_MAX_LAYERS];   // [2*4H][Din]  row-major, gate-interleaved rows
+  size_t enc_bias[CASR_MAX_LAYERS];  // [2*4H]       b_ih + b_hh, same row order
+  size_t enc_whh[CASR_MAX_LAYERS];   // frag-major [2][H/16][4][H/64]
+  size_t emb;                        // [V][E]
+  size_t dec_w;                      // frag-major [HD/16][4][KDEC/64]
+  size_t dec_b;                      // [4HD] gate-interleaved
+  size_t proj_w;                     // frag-major [VP/64 * 4][KPROJ/64], k order [ctx | h]
+  size_t proj_b;                     // [VP]
+  size_t wencT;                      // [A][C]
+  size_t b_attn;                     // [A]
+  size_t w_hidden;                   // [HD][A]
+  size_t v;                          // [A]
+  size_t total;
+  int layers, V, VP;
+};
+
+Layout make_layout(const casr_config& cfg);
+
+// Packed row index of (gate g, unit u) for a gate-interleaved LSTM matrix with hidden
+// size n_hidden: blocks of 16 units, each block = 4 gates x 16 units.
+inline int packed_gate_row(int g, int u) { return (u / 16) * 64 + g * 16 + (u % 16); }
+
+// ---------------------------------------------------------------- launch timing
+// Event pairs around launches of enabled kernel classes (casr_profile_enable).
+struct Profiler {
+  uint32_t mask = 0;
+  std::vector<hipEvent_t> ev[CASR_K_COUNT];
+  size_t used[CASR_K_COUNT] = {};
+  void mark(int cls, hipStream_t s) {
+    if (!((mask >> cls) & 1u)) return;
+    if (used[cls] == ev[cls].size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      ev[cls].push_back(e);
+    }
+    (void)hipEventRecord(ev[cls][used[cls]++], s);
+  }
+  void reset() {
+    for (int c = 0; c < CASR_K_COUNT; ++c) used[c] = 0;
+  }
+  ~Profiler() {
+    for (auto& v : ev)
+      for (hipEvent_t e : v) (void)hipEventDestroy(e);
+  }
+};
+
+// RAII begin/end marker
+struct ProfScope {
+  Profiler* p;
+  int cls;
+  hipStream_t s;
+  ProfScope(Profiler* p_, int c, hipStream_t s_) : p(p_), cls(c), s(s_) {
+    if (p) p->mark(cls, s);
+  }
+  ~ProfScope() {
+    if (p) p->mark(cls, s);
+  }
+};
+
+// ---------------------------------------------------------------- kernel launchers
+// features.hip
+hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int T, float eps,
+                           float* feat, int32_t* feat_len, hipStream_t s);
+hipError_t launch_gather_utts(const float* const* ptrs, const int32_t* lens, int B, int Tp,
+                              float* feat, hipStream_t s);
+
+// encoder.hip
+hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, const float* bias,
+                             float* Gin, hipStream_t s);
+hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
+                           const float* hprev, float* hnext, float* cst, float* hfin,
+                           const int32_t* lens, int B, int Tp, int step, int residual, hipStream_t s);
+hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
+                       float* keysT, hipStream_t s);
+
+// decoder.hip
+struct DecodeBufs {
+  float* st[2];          // [R][ST]
+  float* logits;         // [R][V]
+  int32_t* tok[2];       // [R]
+  int32_t* src[2];       // [R]
+  float* score[2];       // [R]
+  int32_t* newdone;      // [max_len] rows/utterances newly finished at each step
+  // greedy
+  uint8_t* fin;          // [R]
+  // beam
+  uint8_t* topfin;       // [B]
+  int32_t* bp;           // [L][R]
+  int32_t* tk;           // [L][R]
+  float* rec_score;      // [B][L][k]
+  int32_t* rec_src;      // [B][L][k]
+  uint8_t* rec_valid;    // [B][L][k]
+};
+
+struct DecodeArgs {
+  const float* W;        // packed blob base
+  Layout L;
+  const float* enc;      // [B][Tp][C]
+  const float* keysT;    // [B][A][Tp]
+  const float* hfin;     // [2][B][H]
+  const float* cfin;     // [2][B][H]
+  const int32_t* lens;   // [B]
+  int B, Tp, k, V, max_len, sos, eos;
+  float temperature;
+  Profiler* prof;        // may be null
+};
+
+hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
+                      uint8_t* finished, float* accum, float* align, hipStream_t s);
+hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float length_weight,
+                    int32_t* best_tokens, int32_t* best_len, float* best_score, int32_t* steps,
+                    hipStream_t s);
+hipError_t run_beam_records(const DecodeArgs& a, DecodeBufs& d, int32_t* rec_tokens,
+                            float* rec_score, uint8_t* rec_valid, hipStream_t s);
+
+}  // namespace casr

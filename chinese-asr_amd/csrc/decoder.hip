@@ -1,0 +1,782 @@
+// Attention decoder + greedy / beam-search loop on gfx950.
+//
+// Per decode step l (R = B*k rows, row r = b*k + j as tile_batch lays them out,
+// util.py:41-56) four launches, all reading only device state:
+//   1. dec_lstm  RNNDecoder.forward cell part (decoder.py:104-114): gates =
+//      [embed(tok) | ctx_prev | h_prev] . [W_ih | W_hh]^T + b  (K = 1280), LSTMCell in the
+//      epilogue.  Beam reordering (model.py:913-926) is an index: row r reads its
+//      predecessor state from row src[r]; nothing is copied.
+//   2. attention BauAttn.forward heads == 1 (attention.py:91-95): one block per utterance
+//      serves its k beams, so each utterance's keys/values are streamed once per step
+//      (the reference re-gathers them per beam: model.py:913-916).
+//   3. proj      logit = [h | ctx] . W_p^T + b (decoder.py:129-135).
+//   4. select    greedy: log-softmax + first-index argmax + the finished/score bookkeeping of
+//      model.py:554-578; beam: top-2k over k*V per utterance with wave shuffles + an LDS
+//      merge and the finished/active rules of model.py:834-929.
+// The GEMMs use v_mfma_f32_16x16x4_f32 (exact fp32) with weights in MFMA-fragment-major
+// order and split-K over the block's 4 waves.  Early exit (model.py:578 / :897-901) is a
+// device-side per-step counter every kernel checks, so the host never synchronises.
+#include <float.h>
+
+#include "casr_common.h"
+#include "casr_internal.h"
+
+namespace casr {
+
+__device__ __forceinline__ int done_before(const int32_t* __restrict__ newdone, int l) {
+  int s = 0;
+  for (int i = 0; i < l; ++i) s += newdone[i];
+  return s;
+}
+
+// ------------------------------------------------------------------ split-K row GEMM
+// Block: 16*TM rows x 64 output columns (4 MFMA n-tiles), 4 waves each own every 4th
+// 64-deep k chunk; partial tiles are summed through LDS.
+template <int TM>
+struct RedTile {
+  f32x4 v[4][TM][4][64];
+  __device__ __forceinline__ float get(int rowl, int coll) const {
+    const int tm = rowl >> 4, rl = rowl & 15, tn = coll >> 4, u = coll & 15;
+    const int ln = u + 16 * (rl >> 2), reg = rl & 3;
+    return ((v[0][tm][tn][ln][reg] + v[1][tm][tn][ln][reg]) + v[2][tm][tn][ln][reg]) +
+           v[3][tm][tn][ln][reg];
+  }
+};
+
+template <int TM, class ASrc, class Epi>
+__global__ __launch_bounds__(256) void rowgemm_kernel(int nkc, const float* __restrict__ Wf,
+                                                      ASrc asrc, Epi epi) {
+  __shared__ RedTile<TM> red;
+  if (epi.skip()) return;
+  const int nb = blockIdx.x, rb = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+
+  f32x4 acc[TM][4];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int kc = w; kc < nkc; kc += 4) {
+    float4 a[TM][4], bw[4][4];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+      const float* ap = asrc.ptr(rb * 16 * TM + tm * 16 + r, kc * 64 + g * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        a[tm][q] = ap ? *reinterpret_cast<const float4*>(ap + q * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const float* wb = Wf + ((size_t)(nb * 4 + tn) * nkc + kc) * FRAG + lane * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bw[tn][q] = *reinterpret_cast<const float4*>(wb + q * 256);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) {
+          acc[tm][tn] = mfma16x16x4(a[tm][q].x, bw[tn][q].x, acc[tm][tn]);
+          acc[tm][tn] = mfma16x16x4(a[tm][q].y, bw[tn][q].y, acc[tm][tn]);
+          acc[tm][tn] = mfma16x16x4(a[tm][q].z, bw[tn][q].z, acc[tm][tn]);
+          acc[tm][tn] = mfma16x16x4(a[tm][q].w, bw[tn][q].w, acc[tm][tn]);
+        }
+  }
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) red.v[w][tm][tn][lane] = acc[tm][tn];
+  __syncthreads();
+  epi.run(red, rb, nb);
+}
+
+// A rows of the decoder LSTM: [embed(tok[r]) | st_old[src[r]][0:1024] = ctx | h]
+struct DecLstmA {
+  const float* emb;
+  const float* st_old;
+  const int32_t* tok;
+  const int32_t* src;
+  int R;
+  __device__ __forceinline__ const float* ptr(int row, int k) const {
+    if (row >= R) return nullptr;
+    if (k < E) return emb + (size_t)tok[row] * E + k;
+    return st_old + (size_t)src[row] * ST + (k - E);
+  }
+};
+
+template <int TM>
+struct DecLstmEpi {
+  const float* bias;  // packed [4HD]
+  const float* st_old;
+  float* st_new;
+  const int32_t* src;
+  const int32_t* newdone;
+  int R, l, total;
+  __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
+  __device__ __forceinline__ void run(const RedTile<TM>& red, int rb, int nb) const {
+    for (int idx = threadIdx.x; idx < 16 * TM * 16; idx += 256) {
+      const int rowl = idx >> 4, u = idx & 15;
+      const int row = rb * 16 * TM + rowl;
+      if (row >= R) continue;
+      float gate[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) gate[g] = red.get(rowl, g * 16 + u) + bias[nb * 64 + g * 16 + u];
+      const int U = nb * 16 + u;
+      float h2, c2;
+      lstm_cell(gate[0], gate[1], gate[2], gate[3], st_old[(size_t)src[row] * ST + C + HD + U], h2, c2);
+      st_new[(size_t)row * ST + C + U] = h2;
+      st_new[(size_t)row * ST + C + HD + U] = c2;
+    }
+  }
+};
+
+struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h]
+  const float* st;
+  int R;
+  __device__ __forceinline__ const float* ptr(int row, int k) const {
+    return row < R ? st + (size_t)row * ST + k : nullptr;
+  }
+};
+
+template <int TM>
+struct ProjEpi {
+  const float* bias;
+  float* logits;
+  const int32_t* newdone;
+  int R, V, l, total;
+  __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
+  __device__ __forceinline__ void run(const RedTile<TM>& red, int rb, int nb) const {
+    for (int idx = threadIdx.x; idx < 16 * TM * 64; idx += 256) {
+      const int rowl = idx >> 6, coll = idx & 63;
+      const int row = rb * 16 * TM + rowl, n = nb * 64 + coll;
+      if (row < R && n < V) logits[(size_t)row * V + n] = red.get(rowl, coll) + bias[n];
+    }
+  }
+};
+
+// ------------------------------------------------------------------ attention
+// One block per utterance b serving its k rows.  Shared: h [k][HD], q [k][A], e/alpha
+// [k][Tp].  keysT is [B][A][Tp] so lanes walking t read coalesced rows.
+template <int KM>
+__global__ __launch_bounds__(256) void attention_kernel(
+    float* __restrict__ st, const float* __restrict__ keysT, const float* __restrict__ enc,
+    const int32_t* __restrict__ lens, const float* __restrict__ Wh, const float* __restrict__ vv,
+    int k, int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l,
+    int total) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (done_before(newdone, l) >= total) return;
+  float* hs = sm;                 // [KM][HD]
+  float* qs = hs + KM * HD;       // [KM][A]
+  float* qp = qs + KM * A;        // [KM][A] partials
+  float* es = qp + KM * A;        // [KM][Tp]
+  __shared__ float wred[2][4][KM];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int len = lens[b];
+
+  // 1. h rows -> LDS
+  for (int i = tid; i < k * HD; i += 256) {
+    const int j = i / HD, c = i - j * HD;
+    hs[j * HD + c] = st[(size_t)(b * k + j) * ST + C + c];
+  }
+  __syncthreads();
+
+  // 2. q = h . W_hidden  (thread: column a, half of the 512-long contraction)
+  {
+    const int a = tid & (A - 1), part = tid >> 7;
+    float acc[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) acc[j] = 0.f;
+    for (int i = part * (HD / 2); i < (part + 1) * (HD / 2); ++i) {
+      const float wv = Wh[(size_t)i * A + a];
+#pragma unroll
+      for (int j = 0; j < KM; ++j)
+        if (j < k) acc[j] = fmaf(hs[j * HD + i], wv, acc[j]);
+    }
+    float* dst = part ? qp : qs;
+#pragma unroll
+    for (int j = 0; j < KM; ++j)
+      if (j < k) dst[j * A + a] = acc[j];
+  }
+  __syncthreads();
+  for (int i = tid; i < k * A; i += 256) qs[i] += qp[i];
+  __syncthreads();
+
+  // 3. scores e[j][t] = sum_a v[a] * tanh(keys[t][a] + q[j][a]); masked past len
+  float lmax[KM];
+#pragma unroll
+  for (int j = 0; j < KM; ++j) lmax[j] = -INFINITY;
+  const float* kb = keysT + (size_t)b * A * Tp;
+  for (int t = tid; t < Tp; t += 256) {
+    float e[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) e[j] = 0.f;
+    if (t < len) {
+      for (int a = 0; a < A; ++a) {
+        const float kv = kb[(size_t)a * Tp + t];
+        const float va = vv[a];
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+          if (j < k) e[j] += tanhf(kv + qs[j * A + a]) * va;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j)
+      if (j < k) {
+        const float ev = (t < len) ? e[j] : -INFINITY;
+        es[j * Tp + t] = ev;
+        lmax[j] = fmaxf(lmax[j], ev);
+      }
+  }
+  // block max per row
+  const int wv_ = tid >> 6, ln = tid & 63;
+#pragma unroll
+  for (int j = 0; j < KM; ++j)
+    if (j < k) {
+      const float m = wave_max(lmax[j]);
+      if (ln == 0) wred[0][wv_][j] = m;
+    }
+  __syncthreads();
+  float rmax[KM], lsum[KM];
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    rmax[j] = (j < k) ? fmaxf(fmaxf(wred[0][0][j], wred[0][1][j]), fmaxf(wred[0][2][j], wred[0][3][j])) : 0.f;
+    lsum[j] = 0.f;
+  }
+  // 4. softmax over t (torch: exp(x - max), then * 1/sum)
+  for (int t = tid; t < Tp; t += 256) {
+#pragma unroll
+    for (int j = 0; j < KM; ++j)
+      if (j < k) {
+        const float p = expf(es[j * Tp + t] - rmax[j]);
+        es[j * Tp + t] = p;
+        lsum[j] += p;
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < KM; ++j)
+    if (j < k) {
+      const float s = wave_sum(lsum[j]);
+      if (ln == 0) wred[1][wv_][j] = s;
+    }
+  __syncthreads();
+  float rinv[KM];
+#pragma unroll
+  for (int j = 0; j < KM; ++j)
+    rinv[j] = (j < k) ? 1.0f / ((wred[1][0][j] + wred[1][1][j]) + (wred[1][2][j] + wred[1][3][j])) : 0.f;
+  for (int t = tid; t < Tp; t += 256) {
+#pragma unroll
+    for (int j = 0; j < KM; ++j)
+      if (j < k) {
+        const float al = es[j * Tp + t] * rinv[j];
+        es[j * Tp + t] = al;
+        if (align) align[(size_t)t * ((size_t)gridDim.x * k) + b * k + j] = al;
+      }
+  }
+  __syncthreads();
+
+  // 5. context ctx[j][c] = sum_t alpha[j][t] * enc[b][t][c]; thread owns 2 columns
+  {
+    const int c0 = 2 * tid;
+    float acc0[KM], acc1[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) acc0[j] = acc1[j] = 0.f;
+    const float* eb = enc + (size_t)b * Tp * C + c0;
+    for (int t = 0; t < len; ++t) {
+      const float2 v2 = *reinterpret_cast<const float2*>(eb + (size_t)t * C);
+#pragma unroll
+      for (int j = 0; j < KM; ++j)
+        if (j < k) {
+          const float al = es[j * Tp + t];
+          acc0[j] += al * v2.x;
+          acc1[j] += al * v2.y;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j)
+      if (j < k) {
+        float* o = st + (size_t)(b * k + j) * ST + c0;
+        o[0] = acc0[j];
+        o[1] = acc1[j];
+      }
+  }
+}
+
+// ------------------------------------------------------------------ init
+// st0[r] = [ctx 0 | h_fin(b) | c_fin(b)], tok = sos, src = r, score = 0 (model.py:531-535,
+// :660-669, :684-690).
+__global__ void decode_init_kernel(float* __restrict__ st0, const float* __restrict__ hfin,
+                                   const float* __restrict__ cfin, int B, int k, int sos,
+                                   int32_t* __restrict__ tok, int32_t* __restrict__ src,
+                                   float* __restrict__ score) {
+  const int r = blockIdx.x, b = r / k;
+  float* o = st0 + (size_t)r * ST;
+  for (int i = threadIdx.x; i < ST; i += blockDim.x) {
+    float v;
+    if (i < C) {
+      v = 0.f;
+    } else if (i < C + HD) {
+      const int u = i - C;  // [fw | bw]
+      v = hfin[((size_t)(u / H) * B + b) * H + (u % H)];
+    } else {
+      const int u = i - C - HD;
+      v = cfin[((size_t)(u / H) * B + b) * H + (u % H)];
+    }
+    o[i] = v;
+  }
+  if (threadIdx.x == 0) {
+    tok[r] = sos;
+    src[r] = r;
+    score[r] = 0.f;
+  }
+}
+
+// ------------------------------------------------------------------ greedy select
+struct ArgMax {
+  float v;
+  int i;
+};
+__device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
+  return av > bv || (av == bv && ai < bi);
+}
+
+__global__ __launch_bounds__(256) void greedy_select_kernel(
+    const float* __restrict__ logits, int V, int R, int l, int L, int eos, int32_t* __restrict__ tok_next,
+    int32_t* __restrict__ src_next, uint8_t* __restrict__ fin, int32_t* __restrict__ out_len, float* __restrict__ accum,
+    int32_t* __restrict__ tokens, int32_t* __restrict__ newdone) {
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  __shared__ float ss[4];
+  if (done_before(newdone, l) >= R) return;
+  const int r = blockIdx.x, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
+  const float* x = logits + (size_t)r * V;
+  float m = -INFINITY;
+  int mi = 0x7fffffff;
+  for (int v = tid; v < V; v += 256) {
+    const float xv = x[v];
+    if (xv > m) {
+      m = xv;
+      mi = v;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(m, o, 64);
+    const int oi = __shfl_xor(mi, o, 64);
+    if (better(ov, oi, m, mi)) {
+      m = ov;
+      mi = oi;
+    }
+  }
+  if (ln == 0) {
+    sv[wv] = m;
+    si[wv] = mi;
+  }
+  __syncthreads();
+  m = sv[0];
+  mi = si[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w)
+    if (better(sv[w], si[w], m, mi)) {
+      m = sv[w];
+      mi = si[w];
+    }
+  float s = 0.f;
+  for (int v = tid; v < V; v += 256) s += expf(x[v] - m);
+  s = wave_sum(s);
+  if (ln == 0) ss[wv] = s;
+  __syncthreads();
+  if (tid == 0) {
+    const float sum = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+    const float lse = logf(sum) + m;  // torch.logsumexp: log(sum(exp(x - max))) + max
+    const float lp = m - lse;
+    const int tok = mi;
+    tokens[(size_t)r * L + l] = tok;
+    tok_next[r] = tok;
+    src_next[r] = r;  // greedy never reorders
+    const bool was = fin[r] != 0;
+    const bool cur = tok == eos;
+    float acc = accum[r];
+    if (!was && cur) acc = acc + lp;  // model.py:567
+    const bool now = was || cur;
+    if (!now) {
+      out_len[r] += 1;  // model.py:573
+      acc = acc + lp;   // model.py:576
+    }
+    accum[r] = acc;
+    if (now && !was) {
+      fin[r] = 1;
+      atomicAdd(&newdone[l], 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ beam select
+template <int K2>
+struct TopList {
+  float v[K2];
+  int i[K2];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int p = 0; p < K2; ++p) {
+      v[p] = -INFINITY;
+      i[p] = 0x7fffffff;
+    }
+  }
+  __device__ __forceinline__ void insert(float xv, int xi) {
+    if (!better(xv, xi, v[K2 - 1], i[K2 - 1])) return;
+    v[K2 - 1] = xv;
+    i[K2 - 1] = xi;
+#pragma unroll
+    for (int p = K2 - 1; p > 0; --p) {
+      if (better(v[p], i[p], v[p - 1], i[p - 1])) {
+        const float tv = v[p];
+        v[p] = v[p - 1];
+        v[p - 1] = tv;
+        const int ti = i[p];
+        i[p] = i[p - 1];
+        i[p - 1] = ti;
+      }
+    }
+  }
+  __device__ __forceinline__ void pop() {
+#pragma unroll
+    for (int p = 0; p < K2 - 1; ++p) {
+      v[p] = v[p + 1];
+      i[p] = i[p + 1];
+    }
+    v[K2 - 1] = -INFINITY;
+    i[K2 - 1] = 0x7fffffff;
+  }
+};
+
+// Extract the top n (<= K2) of the union of the 64 lanes' sorted lists; lane 0 writes them.
+template <int K2>
+__device__ __forceinline__ void wave_merge(TopList<K2>& L, int n, float* outv, int* outi) {
+  for (int c = 0; c < n; ++c) {
+    float bv = L.v[0];
+    int bi = L.i[0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (better(ov, oi, bv, bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (L.i[0] == bi && L.v[0] == bv) L.pop();
+    if ((threadIdx.x & 63) == 0) {
+      outv[c] = bv;
+      outi[c] = bi;
+    }
+  }
+}
+
+template <int K2>
+__global__ __launch_bounds__(256) void beam_select_kernel(
+    const float* __restrict__ logits, int V, int B, int k, int l, int L, int eos, float temperature,
+    const float* __restrict__ score_cur, float* __restrict__ score_next,
+    int32_t* __restrict__ tok_next, int32_t* __restrict__ src_next, uint8_t* __restrict__ topfin,
+    int32_t* __restrict__ bp, int32_t* __restrict__ tk, float* __restrict__ rec_score,
+    int32_t* __restrict__ rec_src, uint8_t* __restrict__ rec_valid, int32_t* __restrict__ newdone) {
+  __shared__ float lse_s[KMAX_BEAM];
+  __shared__ float wv_s[4][K2];
+  __shared__ int wi_s[4][K2];
+  __shared__ float cv[K2];
+  __shared__ int ci[K2];
+  if (done_before(newdone, l) >= B) return;
+  const int b = blockIdx.x, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
+  const int R = B * k;
+  const int nrows = (l == 0) ? 1 : k;  // model.py:862-863: step 0 ranks beam 0 only
+  const int n2k = 2 * k;
+
+  for (int j = wv; j < nrows; j += 4) {
+    const float* x = logits + (size_t)(b * k + j) * V;
+    float m = -INFINITY;
+    for (int v = ln; v < V; v += 64) m = fmaxf(m, x[v] / temperature);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int v = ln; v < V; v += 64) s += expf(x[v] / temperature - m);
+    s = wave_sum(s);
+    if (ln == 0) lse_s[j] = logf(s) + m;
+  }
+  __syncthreads();
+
+  TopList<K2> tl;
+  tl.init();
+  for (int j = 0; j < nrows; ++j) {
+    const float* x = logits + (size_t)(b * k + j) * V;
+    const float lse = lse_s[j], sc = score_cur[b * k + j];
+    for (int v = tid; v < V; v += 256) {
+      const float val = (x[v] / temperature - lse) + sc;  // model.py:834-836
+      tl.insert(val, j * V + v);
+    }
+  }
+  wave_merge<K2>(tl, n2k, wv_s[wv], wi_s[wv]);
+  __syncthreads();
+  if (wv == 0) {
+    TopList<K2> t2;
+    t2.init();
+    for (int p = ln; p < 4 * n2k; p += 64) t2.insert(wv_s[p / n2k][p % n2k], wi_s[p / n2k][p % n2k]);
+    wave_merge<K2>(t2, n2k, cv, ci);
+  }
+  __syncthreads();
+
+  if (tid == 0) {
+    // finished hypotheses among the first k candidates (model.py:874-889)
+    for (int c = 0; c < k; ++c) {
+      const int beam = ci[c] / V, tok = ci[c] - beam * V;
+      const size_t ri = ((size_t)b * L + l) * k + c;
+      const bool f = tok == eos;
+      rec_valid[ri] = f;
+      if (f) {
+        rec_score[ri] = cv[c];
+        rec_src[ri] = beam;
+      }
+    }
+    const int tok0 = ci[0] % V;
+    if (!topfin[b] && tok0 == eos) {  // model.py:897-901
+      topfin[b] = 1;
+      atomicAdd(&newdone[l], 1);
+    }
+    // active = first k non-EOS candidates in rank order (model.py:904-909)
+    int na = 0;
+    for (int pass = 0; pass < 2 && na < k; ++pass)
+      for (int c = 0; c < n2k && na < k; ++c) {
+        const int beam = ci[c] / V, tok = ci[c] - beam * V;
+        if ((tok == eos) != (pass == 1)) continue;
+        const int row = b * k + na;
+        tok_next[row] = tok;
+        src_next[row] = b * k + beam;
+        score_next[row] = cv[c];
+        bp[(size_t)l * R + row] = beam;
+        tk[(size_t)l * R + row] = tok;
+        ++na;
+      }
+  }
+}
+
+// executed loop steps: the step at which the cumulative count reached `total`, + 1
+__device__ __forceinline__ int executed_steps(const int32_t* newdone, int L, int total) {
+  int cum = 0;
+  for (int s = 0; s < L; ++s) {
+    cum += newdone[s];
+    if (cum >= total) return s + 1;
+  }
+  return L;
+}
+
+// one thread per utterance: first-max finished record (model.py:765) or the unfinished
+// fallback (model.py:961-972); tokens recovered by walking the back-pointers.
+__global__ void beam_finalize_kernel(int B, int k, int L, float lm_weight, float length_weight,
+                                     const float* __restrict__ score0,
+                                     const float* __restrict__ score1,
+                                     const int32_t* __restrict__ bp, const int32_t* __restrict__ tk,
+                                     const float* __restrict__ rec_score,
+                                     const int32_t* __restrict__ rec_src,
+                                     const uint8_t* __restrict__ rec_valid,
+                                     const int32_t* __restrict__ newdone, int32_t* __restrict__ best_tokens,
+                                     int32_t* __restrict__ best_len, float* __restrict__ best_score,
+                                     int32_t* __restrict__ steps_out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  const int steps = executed_steps(newdone, L, B);
+  if (b == 0) steps_out[0] = steps;
+  if (b >= B) return;
+  const int R = B * k;
+  // the select of step l writes score[(l+1)&1]; the last executed step is steps-1
+  const float* score_final = (steps & 1) ? score1 : score0;
+  int bl = -1, bc = -1;
+  float bs = 0.f;
+  for (int l = 0; l < steps; ++l)
+    for (int c = 0; c < k; ++c) {
+      const size_t ri = ((size_t)b * L + l) * k + c;
+      if (rec_valid[ri] && (bl < 0 || rec_score[ri] > bs)) {
+        bl = l;
+        bc = c;
+        bs = rec_score[ri];
+      }
+    }
+  int32_t* out = best_tokens + (size_t)b * L;
+  int len, slot, from;
+  if (bl >= 0) {
+    len = bl;
+    slot = rec_src[((size_t)b * L + bl) * k + bc];
+    from = bl - 1;
+  } else {
+    const int ll = steps - 1;
+    const float lw = (float)((double)length_weight * (double)(ll + 1));
+    int bj = 0;
+    float bsv = 0.f;
+    for (int j = 0; j < k; ++j) {
+      const float s = (score_final[b * k + j] + lm_weight * 0.f) + lw;
+      if (j == 0 || s > bsv) {
+        bsv = s;
+        bj = j;
+      }
+    }
+    bs = bsv;
+    len = ll + 1;
+    slot = bj;
+    from = ll;
+  }
+  for (int s = from; s >= 0; --s) {
+    const size_t ix = (size_t)s * R + b * k + slot;
+    out[s] = tk[ix];
+    slot = bp[ix];
+  }
+  for (int s = len; s < L; ++s) out[s] = -1;
+  best_len[b] = len;
+  best_score[b] = bs;
+}
+
+// grid (B, L), block 64: expand every finished record's token sequence.
+__global__ void beam_records_kernel(int B, int k, int L, const int32_t* __restrict__ bp,
+                                    const int32_t* __restrict__ tk, const float* __restrict__ rec_score,
+                                    const int32_t* __restrict__ rec_src,
+                                    const uint8_t* __restrict__ rec_valid,
+                                    const int32_t* __restrict__ newdone, int32_t* __restrict__ out_tok,
+                                    float* __restrict__ out_score, uint8_t* __restrict__ out_valid) {
+  const int b = blockIdx.x, l = blockIdx.y, c = threadIdx.x;
+  if (c >= k) return;
+  const int steps = executed_steps(newdone, L, B);
+  const size_t ri = ((size_t)b * L + l) * k + c;
+  const bool valid = l < steps && rec_valid[ri];
+  out_valid[ri] = valid;
+  int32_t* o = out_tok + ri * L;
+  if (!valid) {
+    for (int s = 0; s < L; ++s) o[s] = -1;
+    out_score[ri] = 0.f;
+    return;
+  }
+  out_score[ri] = rec_score[ri];
+  int slot = rec_src[ri];
+  const int R = B * k;
+  for (int s = l - 1; s >= 0; --s) {
+    const size_t ix = (size_t)s * R + b * k + slot;
+    o[s] = tk[ix];
+    slot = bp[ix];
+  }
+  for (int s = l; s < L; ++s) o[s] = -1;
+}
+
+// ------------------------------------------------------------------ host drivers
+template <int KM>
+static hipError_t launch_attention(const DecodeArgs& a, float* st, float* align, int32_t* newdone,
+                                   int l, int total, hipStream_t s) {
+  const size_t shm = (size_t)(KM * HD + 2 * KM * A + KM * a.Tp) * sizeof(float);
+  hipLaunchKernelGGL(attention_kernel<KM>, dim3(a.B), dim3(256), shm, s, st, a.keysT, a.enc, a.lens,
+                     a.W + a.L.w_hidden, a.W + a.L.v, a.k, a.Tp, align, newdone, l, total);
+  return hipGetLastError();
+}
+
+static hipError_t attention_dispatch(const DecodeArgs& a, float* st, float* align, int32_t* newdone,
+                                     int l, int total, hipStream_t s) {
+  if (a.k <= 1) return launch_attention<1>(a, st, align, newdone, l, total, s);
+  if (a.k <= 4) return launch_attention<4>(a, st, align, newdone, l, total, s);
+  if (a.k <= 8) return launch_attention<8>(a, st, align, newdone, l, total, s);
+  return launch_attention<16>(a, st, align, newdone, l, total, s);
+}
+
+size_t attention_smem_bytes(int k, int Tp) {
+  const int km = k <= 1 ? 1 : k <= 4 ? 4 : k <= 8 ? 8 : 16;
+  return (size_t)(km * HD + 2 * km * A + km * Tp) * sizeof(float);
+}
+
+static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
+                              hipStream_t s) {
+  const int R = a.B * a.k;
+  const float* st_old = d.st[l & 1];
+  float* st_new = d.st[(l + 1) & 1];
+  {
+    ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
+    constexpr int TM = 1;
+    DecLstmA asrc{a.W + a.L.emb, st_old, d.tok[l & 1], d.src[l & 1], R};
+    DecLstmEpi<TM> epi{a.W + a.L.dec_b, st_old, st_new, d.src[l & 1], d.newdone, R, l, total};
+    dim3 grid(HD / 16, (R + 16 * TM - 1) / (16 * TM));
+    hipLaunchKernelGGL((rowgemm_kernel<TM, DecLstmA, DecLstmEpi<TM>>), grid, dim3(256), 0, s,
+                       KDEC / 64, a.W + a.L.dec_w, asrc, epi);
+  }
+  hipError_t e;
+  {
+    ProfScope ps(a.prof, CASR_K_ATTENTION, s);
+    e = attention_dispatch(a, st_new, align, d.newdone, l, total, s);
+  }
+  if (e != hipSuccess) return e;
+  {
+    ProfScope ps(a.prof, CASR_K_PROJ, s);
+    constexpr int TM = 2;
+    ProjA asrc{st_new, R};
+    ProjEpi<TM> epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total};
+    dim3 grid(a.L.VP / 64, (R + 16 * TM - 1) / (16 * TM));
+    hipLaunchKernelGGL((rowgemm_kernel<TM, ProjA, ProjEpi<TM>>), grid, dim3(256), 0, s, KPROJ / 64,
+                       a.W + a.L.proj_w, asrc, epi);
+  }
+  return hipGetLastError();
+}
+
+hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
+                      uint8_t* finished, float* accum, float* align, hipStream_t s) {
+  const int R = a.B;
+  hipError_t e0 = hipMemsetAsync(d.newdone, 0, sizeof(int32_t) * a.max_len, s);
+  if (e0 == hipSuccess) e0 = hipMemsetAsync(finished, 0, R, s);
+  if (e0 == hipSuccess) e0 = hipMemsetAsync(out_len, 0, sizeof(int32_t) * R, s);
+  if (e0 == hipSuccess) e0 = hipMemsetAsync(accum, 0, sizeof(float) * R, s);
+  if (e0 == hipSuccess) e0 = hipMemsetAsync(tokens, 0xff, sizeof(int32_t) * R * a.max_len, s);
+  if (e0 != hipSuccess) return e0;
+  hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, 1,
+                     a.sos, d.tok[0], d.src[0], d.score[0]);
+  for (int l = 0; l < a.max_len; ++l) {
+    hipError_t e = decode_step(a, d, l, R, align ? align + (size_t)l * a.Tp * R : nullptr, s);
+    if (e != hipSuccess) return e;
+    ProfScope ps(a.prof, CASR_K_SELECT, s);
+    hipLaunchKernelGGL(greedy_select_kernel, dim3(R), dim3(256), 0, s, d.logits, a.V, R, l,
+                       a.max_len, a.eos, d.tok[(l + 1) & 1], d.src[(l + 1) & 1], finished, out_len,
+                       accum, tokens, d.newdone);
+  }
+  return hipGetLastError();
+}
+
+template <int K2>
+static void launch_beam_select(const DecodeArgs& a, DecodeBufs& d, int l, hipStream_t s) {
+  hipLaunchKernelGGL(beam_select_kernel<K2>, dim3(a.B), dim3(256), 0, s, d.logits, a.V, a.B, a.k, l,
+                     a.max_len, a.eos, a.temperature, d.score[l & 1], d.score[(l + 1) & 1],
+                     d.tok[(l + 1) & 1], d.src[(l + 1) & 1], d.topfin, d.bp, d.tk, d.rec_score,
+                     d.rec_src, d.rec_valid, d.newdone);
+}
+
+hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float length_weight,
+                    int32_t* best_tokens, int32_t* best_len, float* best_score, int32_t* steps,
+                    hipStream_t s) {
+  const int R = a.B * a.k;
+  hipError_t e0 = hipMemsetAsync(d.newdone, 0, sizeof(int32_t) * a.max_len, s);
+  if (e0 == hipSuccess) e0 = hipMemsetAsync(d.topfin, 0, a.B, s);
+  if (e0 != hipSuccess) return e0;
+  hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, a.k,
+                     a.sos, d.tok[0], d.src[0], d.score[0]);
+  for (int l = 0; l < a.max_len; ++l) {
+    hipError_t e = decode_step(a, d, l, a.B, nullptr, s);
+    if (e != hipSuccess) return e;
+    ProfScope ps(a.prof, CASR_K_SELECT, s);
+    if (a.k <= 2) launch_beam_select<4>(a, d, l, s);
+    else if (a.k <= 4) launch_beam_select<8>(a, d, l, s);
+    else if (a.k <= 8) launch_beam_select<16>(a, d, l, s);
+    else launch_beam_select<32>(a, d, l, s);
+  }
+  hipLaunchKernelGGL(beam_finalize_kernel, dim3((a.B + 63) / 64), dim3(64), 0, s, a.B, a.k, a.max_len,
+                     lm_weight, length_weight, d.score[0], d.score[1], d.bp, d.tk, d.rec_score, d.rec_src,
+                     d.rec_valid, d.newdone, best_tokens, best_len, best_score, steps);
+  return hipGetLastError();
+}
+
+hipError_t run_beam_records(const DecodeArgs& a, DecodeBufs& d, int32_t* rec_tokens,
+                            float* rec_score, uint8_t* rec_valid, hipStream_t s) {
+  hipLaunchKernelGGL(beam_records_kernel, dim3(a.B, a.max_len), dim3(64), 0, s, a.B, a.k, a.max_len,
+                     d.bp, d.tk, d.rec_score, d.rec_src, d.rec_valid, d.newdone, rec_tokens,
+                     rec_score, rec_valid);
+  return hipGetLastError();
+}
+
+}  // namespace casr

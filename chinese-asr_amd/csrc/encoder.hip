@@ -1,0 +1,237 @@
+// BiLSTM encoder on gfx950 (RNNEncoder.forward encoder.py:36-81, RNN_RES.forward
+// util.py:1223-1324) and the attention key projection (BauAttn.compute_key_value,
+// attention.py:67-78).
+//
+// Layout in HBM: batch-major rows (b*Tp + t).
+//   * input projection of a layer: one fp32 MFMA GEMM over all B*Tp rows for both
+//     directions, Gin[b*Tp+t][d*4H + packed(g,u)] = x . W_ih^T + (b_ih + b_hh)
+//     (128x128 LDS-tiled, v_mfma_f32_16x16x4_f32, exact f32);
+//   * recurrence: one launch per time step for both directions.  Each block owns
+//     16 batch rows x 16 hidden units (x 4 gates) of one direction; its 4 waves split the
+//     K = H contraction, read W_hh in MFMA-fragment-major order (one coalesced 1 KiB load
+//     per wave instruction) and h_{t-1} straight into VGPRs, reduce through LDS and apply
+//     the LSTM cell in the epilogue.  Packed-sequence semantics per row: forward step s
+//     processes t = s, backward processes t = len_b - 1 - s, rows with s >= len_b are
+//     untouched; the residual x + y (layers > 0) is fused into the output store.
+#include "casr_common.h"
+#include "casr_internal.h"
+
+namespace casr {
+
+// ------------------------------------------------------------------ big NT GEMM
+// C[M][N] = epilogue(A[M][K] . W[N][K]^T); 256 threads, 128x128 tile, BK = 32, 2x2 waves of
+// 64x64 (4x4 MFMA tiles).  The k order inside a BK tile is permuted identically for A and
+// W (lane group g takes k = 8g + 4*half + e) so each lane's A/W fragment is a contiguous
+// float4 in LDS (ds_read_b128).  Row stride LDK = 36 floats keeps the reads ~conflict-free.
+constexpr int GB_M = 128, GB_N = 128, GB_K = 32, GB_LDK = GB_K + 4;
+
+struct StoreBiasEpi {  // C[row][col] = acc + bias[col]
+  float* C;
+  const float* bias;
+  int ldc;
+  __device__ __forceinline__ void operator()(int row, int col, float v) const {
+    C[(size_t)row * ldc + col] = v + bias[col];
+  }
+};
+
+struct KeysEpi {  // keysT[b][a][t] = acc + b_attn[a], row = b*Tp + t
+  float* keysT;
+  const float* bias;
+  int Tp;
+  __device__ __forceinline__ void operator()(int row, int col, float v) const {
+    const int b = row / Tp, t = row - b * Tp;
+    keysT[((size_t)b * A + col) * Tp + t] = v + bias[col];
+  }
+};
+
+template <class Epi>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ Amat, int lda,
+                                                      const float* __restrict__ Wmat, int ldw,
+                                                      int M, int N, int K, Epi epi) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * (GB_M + GB_N) * GB_LDK];
+  constexpr int STAGE = (GB_M + GB_N) * GB_LDK;  // one buffer: A tile then W tile
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * GB_M, n0 = blockIdx.x * GB_N;
+  const int r = lane & 15, g = lane >> 4;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 ra[4], rw[4];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx >> 3, c4 = idx & 7;
+      const int kk = k0 + c4 * 4;
+      const int ar = m0 + row, wr = n0 + row;
+      ra[i] = (ar < M && kk < K) ? *reinterpret_cast<const float4*>(Amat + (size_t)ar * lda + kk)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      rw[i] = (wr < N && kk < K) ? *reinterpret_cast<const float4*>(Wmat + (size_t)wr * ldw + kk)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx >> 3, c4 = idx & 7;
+      *reinterpret_cast<float4*>(smem + buf * STAGE + row * GB_LDK + c4 * 4) = ra[i];
+      *reinterpret_cast<float4*>(smem + buf * STAGE + (GB_M + row) * GB_LDK + c4 * 4) = rw[i];
+    }
+  };
+
+  const int nk = (K + GB_K - 1) / GB_K;
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * GB_K);
+    const float* as = smem + cur * STAGE;
+    const float* ws = as + GB_M * GB_LDK;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      float4 a[4], w[4];
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+        a[tm] = *reinterpret_cast<const float4*>(as + (wm * 64 + tm * 16 + r) * GB_LDK + g * 8 + half * 4);
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn)
+        w[tn] = *reinterpret_cast<const float4*>(ws + (wn * 64 + tn * 16 + r) * GB_LDK + g * 8 + half * 4);
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) {
+          acc[tm][tn] = mfma16x16x4(a[tm].x, w[tn].x, acc[tm][tn]);
+          acc[tm][tn] = mfma16x16x4(a[tm].y, w[tn].y, acc[tm][tn]);
+          acc[tm][tn] = mfma16x16x4(a[tm].z, w[tn].z, acc[tm][tn]);
+          acc[tm][tn] = mfma16x16x4(a[tm].w, w[tn].w, acc[tm][tn]);
+        }
+    }
+    if (kt + 1 < nk) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const int col = n0 + wn * 64 + tn * 16 + r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wm * 64 + tm * 16 + g * 4 + e;
+        if (row < M && col < N) epi(row, col, acc[tm][tn][e]);
+      }
+    }
+}
+
+hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, const float* bias,
+                             float* Gin, hipStream_t s) {
+  const int N = 8 * H;
+  StoreBiasEpi epi{Gin, bias, N};
+  dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M);
+  hipLaunchKernelGGL(gemm_nt_kernel<StoreBiasEpi>, grid, dim3(256), 0, s, X, Din, W, Din, M, N,
+                     Din, epi);
+  return hipGetLastError();
+}
+
+hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
+                       float* keysT, hipStream_t s) {
+  const int M = B * Tp;
+  KeysEpi epi{keysT, b_attn, Tp};
+  dim3 grid(A / GB_N, (M + GB_M - 1) / GB_M);
+  hipLaunchKernelGGL(gemm_nt_kernel<KeysEpi>, grid, dim3(256), 0, s, enc, C, wencT, C, M, A, C,
+                     epi);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ recurrence step
+// grid (H/16 unit blocks, ceil(B/16) row blocks, 2 directions), block 256.
+__global__ __launch_bounds__(256) void rec_step_kernel(
+    const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
+    float* __restrict__ out, const float* __restrict__ hprev, float* __restrict__ hnext,
+    float* __restrict__ cst, float* __restrict__ hfin, const int32_t* __restrict__ lens, int B,
+    int Tp, int step, int residual) {
+  constexpr int NKC = H / 64;  // k chunks of 64
+  __shared__ f32x4 red[4][4][64];
+  const int jb = blockIdx.x, rb = blockIdx.y, d = blockIdx.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const float* Wd = Whh_f + (size_t)d * (H / 16) * 4 * NKC * FRAG;
+
+  f32x4 acc[4];
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) acc[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int row = rb * 16 + r;
+  for (int kc = w; kc < NKC; kc += 4) {
+    float4 a[4], bw[4][4];
+    const float* ap = hprev + ((size_t)d * B + row) * H + kc * 64 + g * 16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      a[q] = row < B ? *reinterpret_cast<const float4*>(ap + q * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const float* wb = Wd + ((size_t)(jb * 4 + tn) * NKC + kc) * FRAG + lane * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bw[tn][q] = *reinterpret_cast<const float4*>(wb + q * 256);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) {
+        acc[tn] = mfma16x16x4(a[q].x, bw[tn][q].x, acc[tn]);
+        acc[tn] = mfma16x16x4(a[q].y, bw[tn][q].y, acc[tn]);
+        acc[tn] = mfma16x16x4(a[q].z, bw[tn][q].z, acc[tn]);
+        acc[tn] = mfma16x16x4(a[q].w, bw[tn][q].w, acc[tn]);
+      }
+  }
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) red[w][tn][lane] = acc[tn];
+  __syncthreads();
+
+  // epilogue: thread -> (row rl, unit u) cell
+  const int rl = threadIdx.x >> 4, u = threadIdx.x & 15;
+  const int b = rb * 16 + rl;
+  if (b >= B) return;
+  const int len = lens[b];
+  if (step >= len) return;
+  const int t = (d == 0) ? step : (len - 1 - step);
+  const int src_lane = u + 16 * (rl >> 2), reg = rl & 3;
+  float gate[4];
+  const float* gin = Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + jb * 64;
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) {
+    float sum = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) sum += red[ww][tn][src_lane][reg];
+    gate[tn] = sum + gin[tn * 16 + u];
+  }
+  const int U = jb * 16 + u;
+  const size_t si = ((size_t)d * B + b) * H + U;
+  float h2, c2;
+  lstm_cell(gate[0], gate[1], gate[2], gate[3], cst[si], h2, c2);
+  cst[si] = c2;
+  hnext[si] = h2;
+  if (step == len - 1) hfin[si] = h2;
+  const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
+  out[oi] = residual ? (h2 + xin[oi]) : h2;
+}
+
+hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
+                           const float* hprev, float* hnext, float* cst, float* hfin,
+                           const int32_t* lens, int B, int Tp, int step, int residual,
+                           hipStream_t s) {
+  dim3 grid(H / 16, (B + 15) / 16, 2);
+  hipLaunchKernelGGL(rec_step_kernel, grid, dim3(256), 0, s, Whh_f, Gin, xin, out, hprev, hnext,
+                     cst, hfin, lens, B, Tp, step, residual);
+  return hipGetLastError();
+}
+
+}  // namespace casr

@@ -1,0 +1,156 @@
+// Feature post-processing on gfx950: fbank [B][T][80] -> encoder input [B][Tp][720].
+//
+// Reference: add_delta_deltas (data.py:129-164: zero-pad 4 frames each side, cross-
+// correlate with [identity, delta, delta-delta] 9-tap filters normalised to unit L2 norm),
+// 3-frame stacking (data.py:242-249: out[j, c*240 + r*80 + m] = F[c, 3j + r, m]) and the
+// per-utterance CMVN of main.py:37 ((x - mean_t) / (std_t,unbiased + eps)).
+//
+// HBM-bound byte work, no MFMA.  Pass 1 (stack kernel) writes the stacked, un-normalised
+// rows with coalesced 720-float stores; pass 2 (cmvn kernel) owns a 64-dimension column
+// slab of one utterance, reduces mean and the centred second moment over time in two
+// sweeps, then normalises in place (the slab is L2-resident between the sweeps).
+#include "casr_common.h"
+#include "casr_internal.h"
+
+namespace casr {
+
+// Filter taps as float32, normalised exactly like data.py:146-148 (float32 division by the
+// float32 L2 norm).  c = 0 is the identity tap.
+struct DeltaTaps {
+  float d1[9];
+  float d2[9];
+};
+
+__device__ __forceinline__ DeltaTaps make_taps() {
+  DeltaTaps t;
+  const float n1 = sqrtf(10.0f);    // 2^2 + 1 + 1 + 2^2
+  const float n2 = sqrtf(198.0f);   // 16+16+1+16+100+16+1+16+16
+  const float r1[9] = {0.f, 0.f, 2.f, 1.f, 0.f, -1.f, -2.f, 0.f, 0.f};
+  const float r2[9] = {4.f, 4.f, 1.f, -4.f, -10.f, -4.f, 1.f, 4.f, 4.f};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    t.d1[i] = r1[i] / n1;
+    t.d2[i] = r2[i] / n2;
+  }
+  return t;
+}
+
+// grid (Tp, B), block 256: one stacked output row per block.
+__global__ __launch_bounds__(256) void stack_kernel(const float* __restrict__ fbank,
+                                                    const int32_t* __restrict__ frames, int T,
+                                                    int Tp, float* __restrict__ feat,
+                                                    int32_t* __restrict__ feat_len) {
+  const int j = blockIdx.x, b = blockIdx.y;
+  const int nf = min(frames[b], T);
+  const int lp = nf / 3;
+  if (j == 0 && threadIdx.x == 0) feat_len[b] = lp;
+  float* out = feat + ((size_t)b * Tp + j) * D;
+  if (j >= lp) {
+    for (int o = threadIdx.x; o < D; o += 256) out[o] = 0.f;
+    return;
+  }
+  const float* x = fbank + (size_t)b * T * F;
+  const DeltaTaps taps = make_taps();
+  for (int o = threadIdx.x; o < D; o += 256) {
+    const int c = o / (3 * F);
+    const int r = (o % (3 * F)) / F;
+    const int m = o % F;
+    const int t = 3 * j + r;
+    float v;
+    if (c == 0) {
+      v = x[(size_t)t * F + m];
+    } else {
+      const float* w = (c == 1) ? taps.d1 : taps.d2;
+      v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int tt = t + k - 4;
+        const float xv = (tt >= 0 && tt < nf) ? x[(size_t)tt * F + m] : 0.f;
+        v = __fadd_rn(v, __fmul_rn(w[k], xv));
+      }
+    }
+    out[o] = v;
+  }
+}
+
+// grid (ceil(D/64), B), block 256 = 64 dims x 4 time phases.
+__global__ __launch_bounds__(256) void cmvn_kernel(float* __restrict__ feat,
+                                                   const int32_t* __restrict__ feat_len, int Tp,
+                                                   float eps) {
+  __shared__ float part[4][64];
+  __shared__ float stat[2][64];
+  const int b = blockIdx.y;
+  const int dcol = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ph = threadIdx.x >> 6;
+  const int n = feat_len[b];
+  const bool valid = dcol < D;
+  float* base = feat + (size_t)b * Tp * D + dcol;
+
+  float s = 0.f;
+  if (valid)
+    for (int t = ph; t < n; t += 4) s += base[(size_t)t * D];
+  part[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0) {
+    const int i = threadIdx.x;
+    stat[0][i] = ((part[0][i] + part[1][i]) + (part[2][i] + part[3][i])) / (float)n;
+  }
+  __syncthreads();
+  const float mean = stat[0][threadIdx.x & 63];
+  float q = 0.f;
+  if (valid)
+    for (int t = ph; t < n; t += 4) {
+      const float dv = base[(size_t)t * D] - mean;
+      q += dv * dv;
+    }
+  part[ph][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (ph == 0) {
+    const int i = threadIdx.x;
+    const float var = ((part[0][i] + part[1][i]) + (part[2][i] + part[3][i])) / (float)(n - 1);
+    stat[1][i] = sqrtf(var) + eps;
+  }
+  __syncthreads();
+  const float den = stat[1][threadIdx.x & 63];
+  if (valid)
+    for (int t = ph; t < n; t += 4) {
+      float* p = base + (size_t)t * D;
+      *p = (*p - mean) / den;
+    }
+}
+
+hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int T, float eps,
+                           float* feat, int32_t* feat_len, hipStream_t s) {
+  const int Tp = T / 3;
+  if (Tp <= 0 || B <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(stack_kernel, dim3(Tp, B), dim3(256), 0, s, fbank, frames, T, Tp, feat,
+                     feat_len);
+  hipLaunchKernelGGL(cmvn_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, feat, feat_len, Tp,
+                     eps);
+  return hipGetLastError();
+}
+
+// grid (Tp, B): copy row j of utterance b (or zeros past its length), 16 B per lane.
+__global__ __launch_bounds__(192) void gather_kernel(const float* const* __restrict__ ptrs,
+                                                     const int32_t* __restrict__ lens, int Tp,
+                                                     float* __restrict__ feat) {
+  const int j = blockIdx.x, b = blockIdx.y;
+  float4* out = reinterpret_cast<float4*>(feat + ((size_t)b * Tp + j) * D);
+  const int i = threadIdx.x;  // D / 4 = 180 float4 per row
+  if (i >= D / 4) return;
+  if (j < lens[b]) {
+    const float4* in = reinterpret_cast<const float4*>(ptrs[b] + (size_t)j * D);
+    out[i] = in[i];
+  } else {
+    out[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+hipError_t launch_gather_utts(const float* const* ptrs, const int32_t* lens, int B, int Tp,
+                              float* feat, hipStream_t s) {
+  if (Tp <= 0 || B <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_kernel, dim3(Tp, B), dim3(192), 0, s, ptrs, lens, Tp, feat);
+  return hipGetLastError();
+}
+
+}  // namespace casr

@@ -1,0 +1,152 @@
+"""Drop-in for the reference ``Model`` (model.py:18-987) on the MI355X path.
+
+Same constructor, ``load``/``save``, ``eval_one_batch_with_greedy`` and
+``eval_one_batch_with_beam`` signatures and ``EvalOutput`` results; the encoder, attention,
+decoder and the decode loops run as HIP kernels behind the casr C-ABI (include/casr.h).
+The reference builds nn.Modules; here ``model.model`` only provides ``eval()`` (main.py:90)
+and ``model.decoder.real_vcb_sz`` (model.py:623) for callers that read them.
+"""
+import numpy as np
+import torch
+
+from gpd import gpd
+from casr.config import config_from_gpd
+from casr.engine import Engine
+from casr.lib import pack_weights
+from casr.results import (EvalOutput, get_wer, greedy_outputs, greedy_steps, records_by_utterance,
+                          second_pass_select)
+from casr.vocab import load_vocab
+from casr.weights import check_state_dicts, load_checkpoint, save_checkpoint, synthetic_state_dicts
+
+
+class _ModuleList(object):
+    """Stands in for ``nn.ModuleList([encoder, decoder])`` (model.py:78-81): inference only."""
+
+    def eval(self):
+        return self
+
+    def train(self, mode=True):
+        if mode:
+            raise NotImplementedError("the MI355X casr path is inference-only")
+        return self
+
+
+class _DecoderInfo(object):
+    def __init__(self, cfg):
+        self.vocab_size = cfg.max_num_words
+        self.real_vcb_sz = cfg.vocab
+        self.hidden_size = cfg.dec_hidden
+        self.embed_dim = cfg.embed_dim
+
+
+class _EncoderInfo(object):
+    def __init__(self, cfg):
+        self.enc_size = cfg.enc_size
+        self.num_directions = 2
+
+
+class Model(object):
+    def __init__(self):
+        self.cfg = config_from_gpd(gpd)
+        if not torch.cuda.is_available():
+            raise RuntimeError("casr Model runs on an MI355X GPU; none is visible")
+        self.device = torch.device('cuda', torch.cuda.current_device())
+        # the reference starts from random init (init_rnn, util.py:90-114); this path starts
+        # from the deterministic synthetic recipe until load() replaces it
+        self.enc_sd, self.dec_sd = synthetic_state_dicts(self.cfg, peaked=False)
+        self.engine = Engine(self.cfg, self.enc_sd, self.dec_sd, device=self.device)
+        self.encoder = _EncoderInfo(self.cfg)
+        self.decoder = _DecoderInfo(self.cfg)
+        self.model = _ModuleList()
+        self.optimizer = None
+        self._default_int2word = None
+
+    # ------------------------------------------------------------------ weights
+    def load_state_dicts(self, enc_sd, dec_sd):
+        check_state_dicts(self.cfg, enc_sd, dec_sd)
+        self.enc_sd, self.dec_sd = enc_sd, dec_sd
+        self.engine.bind(pack_weights(self.cfg, enc_sd, dec_sd))
+
+    def load(self, path):
+        """model.py:357-370."""
+        if gpd['verbose']:
+            print(f'[INFO] Loading weights from {path}...', end='')
+        enc_sd, dec_sd, args = load_checkpoint(path)
+        self.load_state_dicts(enc_sd, dec_sd)
+        if gpd['verbose']:
+            print(' Loading done.')
+        return args
+
+    def save(self, args, path):
+        """model.py:347-355."""
+        save_checkpoint(path, self.enc_sd, self.dec_sd, args)
+
+    # ------------------------------------------------------------------ helpers
+    def _int2word(self, int2word):
+        if int2word is not None:
+            return int2word
+        if self._default_int2word is None:
+            self._default_int2word = load_vocab()[1]
+        return self._default_int2word
+
+    def _encode(self, data, lens):
+        lens = torch.as_tensor(lens)
+        if isinstance(data, (list, tuple)):
+            feat, lens_d = self.engine.gather(list(data), lens)
+        else:  # already padded [B, Tp, feat_dim]
+            feat, lens_d = data.to(self.device, torch.float32), lens.to(self.device, torch.int32)
+        self.engine.encode(feat, lens_d)
+        return feat.shape[0], lens
+
+    # ------------------------------------------------------------------ decode
+    @torch.no_grad()
+    def eval_one_batch_with_greedy(self, device, data, lens, int2word=None, text=None):
+        """model.py:503-602."""
+        self.model.eval()
+        bsz, lens = self._encode(data, lens)
+        out = self.engine.greedy(alignment=True)
+        tokens = out['tokens'].cpu().numpy()
+        out_len = out['out_len'].cpu().numpy()
+        fin = out['finished'].cpu().numpy().astype(bool)
+        accum = out['accum'].cpu().numpy()
+        toks, score = greedy_outputs(tokens, out_len, fin, accum)
+        steps = greedy_steps(out_len, fin, self.cfg.max_len)
+        alignments = [out['alignment'][l] for l in range(steps)]
+        i2w = self._int2word(int2word)
+        pred_text = ['' if len(t) == 0 else ''.join([i2w[e] for e in t]) for t in toks]
+        wer = None
+        if text is not None:
+            text = [''.join([i2w[e] for e in ele]) for ele in text]
+            wer = np.mean([get_wer(p, r) for p, r in zip(pred_text, text)])
+        return EvalOutput(pred_text=pred_text, score=score, text=text, wer=wer, n=bsz, alignment=alignments,
+                          audio_feat_len=lens, text_len=out['out_len'])
+
+    @torch.no_grad()
+    def eval_one_batch_with_beam(self, device, bmsz, data, lens, text, int2word,
+                                 second_pass=gpd['second_pass'], lm_model=None,
+                                 lm_weight=gpd['lm_weight'], length_weight=gpd['length_weight']):
+        """model.py:604-987."""
+        self.model.eval()
+        bsz, _ = self._encode(data, lens)
+        r = self.engine.beam(bmsz, lm_weight, length_weight)
+        toks = r['tokens'].cpu().numpy()
+        blen = r['length'].cpu().numpy()
+        bscore = r['score'].cpu().numpy()
+        best = {b: (toks[b, :blen[b]].tolist(), float(bscore[b])) for b in range(bsz)}
+        i2w = self._int2word(int2word)
+        if second_pass:
+            rt, rs, rv = (x.cpu().numpy() for x in self.engine.beam_records())
+            recs = records_by_utterance(rt, rs, rv)
+            if lm_model is None and any(len(v) > 1 for v in recs.values()):
+                # the reference calls lm_model.score here (model.py:755) and fails
+                raise AttributeError("second_pass=True needs lm_model ('NoneType' object has no attribute 'score')")
+            best.update(second_pass_select(recs, i2w, lm_model, lm_weight, length_weight))
+        pred_text = [''.join([i2w[idx] for idx in best[b][0]]) for b in range(bsz)]
+        score = [best[b][1] for b in range(bsz)]
+        if text is not None:
+            text = [''.join([i2w[idx] for idx in ele]) for ele in text]
+        wer = None
+        if text is not None:
+            wer = np.mean([get_wer(p, t) for p, t in zip(pred_text, text)])
+        return EvalOutput(pred_text=pred_text, score=score, text=text, wer=wer, n=bsz, alignment=None,
+                          audio_feat_len=None, text_len=None)

@@ -1,0 +1,164 @@
+/*
+ * casr.h — C ABI of the MI355X (gfx950) inference path for the shawnthu/chinese-asr
+ * attention seq2seq model: fbank features -> 4-layer BiLSTM encoder -> Bahdanau
+ * attention -> LSTM decoder -> greedy / beam-search decode loop.
+ *
+ * The reference has no FFI: its boundary is the Python method surface of `Model`
+ * (model.py:18-987) and `main.py` (main.py:27-102).  Each entry point below names the
+ * reference function it replaces; the Python host layer (chinese-asr_amd/model.py,
+ * main.py, data.py) binds them with ctypes and keeps the reference signatures.
+ *
+ * Conventions
+ *   - every function returns CASR_OK (0) or an error code; casr_last_error() explains;
+ *   - all tensor arguments are DEVICE pointers owned by the caller, float32 / int32,
+ *     C-contiguous, unless a comment says "host";
+ *   - `stream` is a hipStream_t passed as void*; no call synchronises the host except
+ *     where noted (the beam/greedy calls return after enqueueing);
+ *   - one handle per device; a handle is not thread-safe; workspaces are owned by the
+ *     handle and grow on demand (first call at a new size allocates).
+ */
+#ifndef CASR_H
+#define CASR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CASR_API_VERSION 1
+#define CASR_MAX_LAYERS 8
+
+enum {
+  CASR_OK = 0,
+  CASR_ERR_ARG = 1,         /* bad argument / shape */
+  CASR_ERR_HIP = 2,         /* HIP runtime error */
+  CASR_ERR_STATE = 3,       /* call order (e.g. decode before encode, no weights) */
+  CASR_ERR_UNSUPPORTED = 4  /* configuration this build does not implement */
+};
+
+typedef struct casr_handle casr_handle;
+
+/* Frozen `gpd` values (gpd.py:13-125), bound at import time in the reference
+ * (encoder.py:17-24, decoder.py:11-16, attention.py:21). */
+typedef struct casr_config {
+  int32_t n_mels;      /* 80   gpd['n_mels'] */
+  int32_t feat_dim;    /* 720  encoder.py:19 (n_mels * 3 * 3) */
+  int32_t enc_hidden;  /* 256  gpd['encoder_hidden_size'] */
+  int32_t enc_layers;  /* 4    gpd['encoder_num_layers'] */
+  int32_t residual;    /* 1    gpd['residual'] (util.py:1284) */
+  int32_t dec_hidden;  /* 512  gpd['decoder_hidden_size'] (must be 2*enc_hidden) */
+  int32_t embed_dim;   /* 256  gpd['embed_dim'] */
+  int32_t attn_size;   /* 128  gpd['attn_size'] */
+  int32_t vocab;       /* 5004 decoder.py:12 real_vcb_sz */
+  int32_t max_len;     /* 40   gpd['max_len'] */
+  int32_t sos;         /* 1 */
+  int32_t eos;         /* 2 */
+  float temperature;   /* gpd['temperature'], model.py:834 (beam only) */
+} casr_config;
+
+/* HOST pointers to the reference state-dict tensors, in their reference layouts
+ * (Model.save, model.py:347-355).  [l][0] = forward, [l][1] = `_reverse`. */
+typedef struct casr_weights_host {
+  const float* enc_w_ih[CASR_MAX_LAYERS][2]; /* rnn.rnn.{l}.weight_ih_l0{,_reverse} [4H][Din] */
+  const float* enc_w_hh[CASR_MAX_LAYERS][2]; /* rnn.rnn.{l}.weight_hh_l0{,_reverse} [4H][H]   */
+  const float* enc_b_ih[CASR_MAX_LAYERS][2]; /* rnn.rnn.{l}.bias_ih_l0{,_reverse}   [4H]      */
+  const float* enc_b_hh[CASR_MAX_LAYERS][2]; /* rnn.rnn.{l}.bias_hh_l0{,_reverse}   [4H]      */
+  const float* embedding;      /* embedding.weight       [V][E]           decoder.py:30 */
+  const float* dec_w_ih;       /* cell.cell.0.weight_ih  [4Hd][E+C]       util.py:1629  */
+  const float* dec_w_hh;       /* cell.cell.0.weight_hh  [4Hd][Hd]                      */
+  const float* dec_b_ih;       /* cell.cell.0.bias_ih    [4Hd]                          */
+  const float* dec_b_hh;       /* cell.cell.0.bias_hh    [4Hd]                          */
+  const float* proj_w;         /* proj_linear.weight     [V][Hd+C]        decoder.py:50 */
+  const float* proj_b;         /* proj_linear.bias       [V]                            */
+  const float* attn_w_enc;     /* attn_mechanism.W_enc   [C][A]           attention.py:28 */
+  const float* attn_b;         /* attn_mechanism.b_attn  [A]                            */
+  const float* attn_w_hidden;  /* attn_mechanism.W_hidden [Hd][A]                       */
+  const float* attn_v;         /* attn_mechanism.v       [A]                            */
+} casr_weights_host;
+
+int casr_api_version(void);
+
+/* Packed weight blob (kernel layouts: gate-interleaved LSTM rows, MFMA-fragment-major
+ * decoder matrices, transposed attention key matrix).  Replaces Model.load's
+ * load_state_dict (model.py:357-370): pack once on the host, upload / broadcast the
+ * blob (RCCL over xGMI for multi-GPU), then bind it on each device. */
+size_t casr_packed_weights_floats(const casr_config* cfg);
+int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float* packed_host);
+
+int casr_create(const casr_config* cfg, int device, casr_handle** out);
+/* Bind a device copy of the packed blob (not copied; must outlive its use). */
+int casr_bind_weights(casr_handle* h, const float* packed_device);
+void casr_destroy(casr_handle* h);
+const char* casr_last_error(const casr_handle* h); /* h may be NULL: last global error */
+
+/* Feature post-processing of a batch of log-mel / fbank frames (data.py:226-249 +
+ * main.py:37 CMVN): 9-tap delta / delta-delta (add_delta_deltas, data.py:129-164),
+ * 3-frame stacking to feat_dim, per-utterance per-dimension (x-mean)/(std_unbiased+eps).
+ *   fbank    [B][T][n_mels]    frames [B] (valid frames per utterance, <= T)
+ *   feat     [B][Tp][feat_dim] with Tp = T/3; rows past frames[b]/3 are zero
+ *   feat_len [B] = frames[b]/3 */
+int casr_features(casr_handle* h, const float* fbank, const int32_t* frames, int B, int T,
+                  float eps, float* feat, int32_t* feat_len, void* stream);
+
+/* The list-of-tensors boundary of Model.eval_one_batch_* (model.py:514-516): gather B
+ * device rows [lens[b]][feat_dim] (utt_ptrs is a DEVICE array of B device pointers) into
+ * the padded batch-major [B][Tp][feat_dim] layout. */
+int casr_gather_utterances(casr_handle* h, const float* const* utt_ptrs, const int32_t* lens,
+                           int B, int Tp, float* feat, void* stream);
+
+/* RNNEncoder.forward (encoder.py:36-81, RNN_RES util.py:1223-1324) + BauAttn
+ * .compute_key_value (attention.py:67-78).  feat [B][Tp][feat_dim], lens [B] (<= Tp).
+ * Results stay in the handle for the following casr_greedy / casr_beam. */
+int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, int Tp, void* stream);
+
+/* Copy of the encoder results (tests / EncoderOutput): enc [B][Tp][2H] (zeros past len),
+ * h_final / c_final [B][2H] (last layer [fw || bw]), keys [B][A][Tp] (any may be NULL). */
+int casr_encoder_results(casr_handle* h, float* enc, float* h_final, float* c_final, float* keys,
+                         void* stream);
+
+/* Model.eval_one_batch_with_greedy decode loop (model.py:527-580) on the last encode.
+ *   tokens   [B][max_len] argmax token of every executed step
+ *   out_len  [B] final_lens (tokens before the first EOS, model.py:573)
+ *   finished [B] 0/1, accum [B] accumulated logp (model.py:567-576)
+ *   align    NULL or [max_len][Tp][B] attention weights per step (model.py:553)
+ * Score = accum / (out_len + finished) is formed by the host (model.py:593). */
+int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* finished, float* accum,
+                float* align, void* stream);
+
+/* Model.eval_one_batch_with_beam search loop (model.py:660-931) + first-max finalize
+ * (model.py:765 / :961-972) for bmsz = k (1..16) on the last encode.
+ *   best_tokens [B][max_len], best_len [B], best_score [B], steps [1] loop steps executed.
+ * With length_weight the unfinished fallback adds length_weight*(l+1) (model.py:964). */
+int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32_t* best_tokens,
+              int32_t* best_len, float* best_score, int32_t* steps, void* stream);
+
+/* Every finished hypothesis of the last casr_beam, for second-pass rescoring on the host
+ * (parse_finished_tensors, model.py:708-765):
+ *   rec_tokens [B][max_len][k][max_len] (record at step l has l tokens), rec_score
+ *   [B][max_len][k], rec_valid [B][max_len][k] (0/1); order = (step, candidate rank). */
+int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uint8_t* rec_valid,
+                      void* stream);
+
+/* Launch timing per kernel class with HIP event pairs recorded on the launch stream around
+ * every launch of the enabled classes (bench.py's roofline figures).  Enabling resets
+ * the counters; reading synchronises on the recorded events. */
+enum {
+  CASR_K_FEATURES = 0,   /* stack + CMVN */
+  CASR_K_INPUT_PROJ = 1, /* encoder input-projection GEMM (per layer) */
+  CASR_K_REC_STEP = 2,   /* one BiLSTM time step (both directions) */
+  CASR_K_KEYS = 3,       /* attention key GEMM */
+  CASR_K_DEC_LSTM = 4,   /* decoder LSTM cell GEMM */
+  CASR_K_ATTENTION = 5,  /* additive attention + context */
+  CASR_K_PROJ = 6,       /* output projection GEMM */
+  CASR_K_SELECT = 7,     /* greedy argmax / beam top-2k + bookkeeping */
+  CASR_K_COUNT = 8
+};
+int casr_profile_enable(casr_handle* h, uint32_t class_mask);
+int casr_profile_read(casr_handle* h, int kernel_class, int32_t* launches, double* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CASR_H */

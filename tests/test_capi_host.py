@@ -1,0 +1,127 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol include/casr.h declares,
+rejects bad configurations, fails loudly without a GPU, and packs weights into the documented
+kernel layouts (checked against a numpy restatement of the layout contract)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from casr import lib as L
+from casr.config import CasrConfig
+from casr.weights import synthetic_state_dicts
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFG = CasrConfig()
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "casr.h")).read()
+    return sorted(set(re.findall(r"\b(casr_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = L.load()
+    declared = header_functions()
+    assert declared == sorted(L.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.casr_api_version() == 1
+
+
+def test_create_without_gpu_or_bad_config_fails_loudly():
+    import torch
+    lib = L.load()
+    h = ctypes.c_void_p()
+    bad = L.config_struct(CFG)
+    bad.enc_hidden = 128
+    assert lib.casr_create(ctypes.byref(bad), 0, ctypes.byref(h)) == 4
+    assert b"enc_hidden" in lib.casr_last_error(None)
+    if not torch.cuda.is_available():
+        c = L.config_struct(CFG)
+        assert lib.casr_create(ctypes.byref(c), 0, ctypes.byref(h)) == 2
+        assert lib.casr_last_error(None)
+    with pytest.raises(L.CasrError):
+        L.check(3)
+
+
+def _layout(cfg):
+    off = 0
+    lay = {}
+
+    def take(name, n):
+        nonlocal off
+        lay[name] = off
+        off += (n + 63) & ~63
+
+    H, C, HD, E, A, D = 256, 512, 512, 256, 128, 720
+    VP = (cfg.vocab + 63) // 64 * 64
+    for l in range(cfg.enc_layers):
+        din = D if l == 0 else C
+        take(f"wih{l}", 8 * H * din)
+        take(f"bias{l}", 8 * H)
+        take(f"whh{l}", 8 * H * H)
+    take("emb", cfg.vocab * E)
+    take("dec_w", 4 * HD * (E + C + HD))
+    take("dec_b", 4 * HD)
+    take("proj_w", VP * (C + HD))
+    take("proj_b", VP)
+    take("wencT", A * C)
+    take("b_attn", A)
+    take("w_hidden", HD * A)
+    take("v", A)
+    lay["total"] = off
+    return lay, VP
+
+
+def _frag(blob, base, nt, kc, nkc, n_local, k_local):
+    """element (row n_local of n-tile nt, k = kc*64 + k_local) of a fragment-major matrix"""
+    g, rem = divmod(k_local, 16)
+    q, e = divmod(rem, 4)
+    lane = n_local + 16 * g
+    return blob[base + (nt * nkc + kc) * 1024 + (q * 64 + lane) * 4 + e]
+
+
+def test_packed_layout_contract():
+    enc, dec = synthetic_state_dicts(CFG)
+    blob = L.pack_weights(CFG, enc, dec)
+    lay, VP = _layout(CFG)
+    assert blob.size == lay["total"]
+    rs = np.random.RandomState(0)
+    H = 256
+    # encoder input projection rows: d*1024 + (u//16)*64 + g*16 + u%16 <- W_ih_d[g*H + u]
+    for l in (0, 2):
+        din = 720 if l == 0 else 512
+        for _ in range(20):
+            d, g, u, k = rs.randint(2), rs.randint(4), rs.randint(H), rs.randint(din)
+            pr = d * 1024 + (u // 16) * 64 + g * 16 + u % 16
+            suf = "_reverse" if d else ""
+            W = enc[f"rnn.rnn.{l}.weight_ih_l0{suf}"]
+            assert blob[lay[f"wih{l}"] + pr * din + k] == W[g * H + u, k]
+            bsum = np.float32(enc[f"rnn.rnn.{l}.bias_ih_l0{suf}"][g * H + u] + enc[f"rnn.rnn.{l}.bias_hh_l0{suf}"][g * H + u])
+            assert blob[lay[f"bias{l}"] + pr] == bsum
+        # recurrent fragments: n-tile jb*4 + g
+        for _ in range(20):
+            d, g, u, k = rs.randint(2), rs.randint(4), rs.randint(H), rs.randint(H)
+            suf = "_reverse" if d else ""
+            W = enc[f"rnn.rnn.{l}.weight_hh_l0{suf}"]
+            jb = u // 16
+            v = _frag(blob, lay[f"whh{l}"] + d * 4 * H * H, jb * 4 + g, k // 64, H // 64, u % 16, k % 64)
+            assert v == W[g * H + u, k]
+    # decoder LSTM fragments, k order [emb | ctx | h]
+    Wih, Whh = dec["cell.cell.0.weight_ih"], dec["cell.cell.0.weight_hh"]
+    for _ in range(40):
+        g, u, k = rs.randint(4), rs.randint(512), rs.randint(1280)
+        want = Wih[g * 512 + u, k] if k < 768 else Whh[g * 512 + u, k - 768]
+        assert _frag(blob, lay["dec_w"], (u // 16) * 4 + g, k // 64, 20, u % 16, k % 64) == want
+    # projection fragments, k order [ctx | h]; rows past V are zero
+    Wp = dec["proj_linear.weight"]
+    for _ in range(40):
+        n, k = rs.randint(VP), rs.randint(1024)
+        want = 0.0 if n >= CFG.vocab else (Wp[n, 512 + k] if k < 512 else Wp[n, k - 512])
+        assert _frag(blob, lay["proj_w"], n // 16, k // 64, 16, n % 16, k % 64) == want
+    np.testing.assert_array_equal(blob[lay["wencT"]:lay["wencT"] + 128 * 512].reshape(128, 512),
+                                  dec["attn_mechanism.W_enc"].T)
+    np.testing.assert_array_equal(blob[lay["emb"]:lay["emb"] + CFG.vocab * 256].reshape(CFG.vocab, 256),
+                                  dec["embedding.weight"])

@@ -1,0 +1,199 @@
+"""HIP path vs the reference (golden vectors) and vs the CPU oracle, through the C ABI.
+
+Tolerances (fp32 everywhere; differences come only from summation order / libm ulps):
+  features 2e-5 abs, encoder outputs 1e-4 abs, beam / greedy scores 2e-3 abs (sums of up to
+  40 log-probs of magnitude <= ~40), attention weights 1e-5 abs; token ids must be identical.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import load_golden, fbank_for, golden_frames
+from oracle import casr_oracle as O
+from stub_lm import StubLM, pua_int2word
+from casr.config import CasrConfig
+from casr.lib import pack_weights
+from casr.results import greedy_outputs, greedy_steps, records_by_utterance, second_pass_select
+from casr.weights import synthetic_state_dicts
+
+pytestmark = pytest.mark.gpu
+
+G, META = load_golden()
+CFG = CasrConfig()
+FRAMES = golden_frames(META)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from casr.engine import Engine
+    e = Engine(CFG, *synthetic_state_dicts(CFG, peaked=False))
+    yield e
+    e.close()
+
+
+def bind(eng, name):
+    eng.bind(pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=(name == "peaked"))))
+
+
+def batch_fbank(frames, dev):
+    T = max(frames)
+    x = np.zeros((len(frames), T, 80), np.float32)
+    for b, t in enumerate(frames):
+        x[b, :t] = fbank_for(b, t)
+    return torch.from_numpy(x).to(dev), torch.tensor(frames, dtype=torch.int32, device=dev)
+
+
+def golden_features(eng):
+    fb, fr = batch_fbank(FRAMES, eng.device)
+    return eng.features(fb, fr, eps=1e-6)
+
+
+def test_features_match_oracle(eng):
+    feat, flen = golden_features(eng)
+    feat = feat.cpu().numpy()
+    assert flen.cpu().tolist() == [t // 3 for t in FRAMES]
+    for b, t in enumerate(FRAMES):
+        ref = O.features_from_fbank(fbank_for(b, t))
+        np.testing.assert_allclose(feat[b, :t // 3], ref, atol=2e-5, rtol=0)
+        assert not feat[b, t // 3:].any()
+    # the reference's own captured features (T=101 utterance 0)
+    fb = torch.from_numpy(fbank_for(0, 101))[None].to(eng.device)
+    f1, _ = eng.features(fb, torch.tensor([101], dtype=torch.int32, device=eng.device))
+    np.testing.assert_allclose(f1[0].cpu().numpy(), G["feat_cmvn_T101"], atol=2e-5, rtol=0)
+
+
+@pytest.mark.parametrize("name", ["plain", "peaked"])
+def test_encoder_matches_reference_and_oracle(eng, name):
+    bind(eng, name)
+    feat, flen = golden_features(eng)
+    eng.encode(feat, flen)
+    enc, h, c, keys = (x.cpu().numpy() for x in eng.encoder_results())
+    np.testing.assert_allclose(h, G[f"{name}_enc_h"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(c, G[f"{name}_enc_c"], atol=1e-4, rtol=0)
+    enc_tm = enc.transpose(1, 0, 2)  # [Tp, B, C] like EncoderOutput.out
+    np.testing.assert_allclose(enc_tm[::7, :, ::64], G[f"{name}_enc_slice"], atol=1e-4, rtol=0)
+    np.testing.assert_allclose(enc.astype(np.float64).sum(axis=(1, 2)), G[f"{name}_enc_sum_per_utt"],
+                               rtol=1e-5, atol=2e-2)
+    # keys over all Tp positions (padding rows hold b_attn), as the reference computes them
+    np.testing.assert_allclose(keys.astype(np.float64).sum(axis=(1, 2)), G[f"{name}_keys_sum_per_utt"],
+                               rtol=1e-5, atol=2e-2)
+
+
+@pytest.mark.parametrize("name", ["plain", "peaked"])
+def test_greedy_matches_reference(eng, name):
+    bind(eng, name)
+    feat, flen = golden_features(eng)
+    eng.encode(feat, flen)
+    out = eng.greedy(alignment=True)
+    tokens = out["tokens"].cpu().numpy()
+    out_len = out["out_len"].cpu().numpy()
+    fin = out["finished"].cpu().numpy().astype(bool)
+    toks, score = greedy_outputs(tokens, out_len, fin, out["accum"].cpu().numpy())
+    gold = META[name]["greedy"]
+    assert toks == gold["tokens"]
+    assert out_len.tolist() == gold["text_len"]
+    assert greedy_steps(out_len, fin, CFG.max_len) == gold["steps"]
+    np.testing.assert_allclose(score, gold["score"], atol=2e-3, rtol=0)
+    align = out["alignment"].cpu().numpy()
+    np.testing.assert_allclose(align[0], G[f"{name}_greedy_align_step0"], atol=1e-5)
+    np.testing.assert_allclose(align[:gold["steps"]].astype(np.float64).sum(1), G[f"{name}_greedy_align_sum"],
+                               atol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["plain", "peaked"])
+@pytest.mark.parametrize("k", [1, 4, 8])
+def test_beam_matches_reference(eng, name, k):
+    bind(eng, name)
+    feat, flen = golden_features(eng)
+    eng.encode(feat, flen)
+    r = eng.beam(k)
+    toks = r["tokens"].cpu().numpy()
+    blen = r["length"].cpu().numpy()
+    gold = META[name][f"beam{k}"]
+    assert [toks[b, :blen[b]].tolist() for b in range(len(FRAMES))] == gold["tokens"]
+    np.testing.assert_allclose(r["score"].cpu().numpy(), gold["score"], atol=2e-3, rtol=0)
+
+
+@pytest.mark.parametrize("name", ["plain", "peaked"])
+def test_beam_second_pass_and_length_weight(eng, name):
+    bind(eng, name)
+    feat, flen = golden_features(eng)
+    eng.encode(feat, flen)
+    r = eng.beam(4, 1.5, 1.5)
+    toks, blen, sc = (x.cpu().numpy() for x in (r["tokens"], r["length"], r["score"]))
+    best = {b: (toks[b, :blen[b]].tolist(), float(sc[b])) for b in range(len(FRAMES))}
+    gold = META[name]["beam4_lw"]
+    assert [best[b][0] for b in range(len(FRAMES))] == gold["tokens"]
+    np.testing.assert_allclose([best[b][1] for b in range(len(FRAMES))], gold["score"], atol=2e-3)
+    recs = records_by_utterance(*(x.cpu().numpy() for x in eng.beam_records()))
+    best.update(second_pass_select(recs, pua_int2word(CFG.vocab), StubLM(), 1.5, 1.5))
+    gold = META[name]["beam4_lm"]
+    assert [best[b][0] for b in range(len(FRAMES))] == gold["tokens"]
+    np.testing.assert_allclose([best[b][1] for b in range(len(FRAMES))], gold["score"], atol=2e-3)
+
+
+def test_model_dropin_api_matches_reference():
+    import model as M
+    m = M.Model()
+    m.load_state_dicts(*synthetic_state_dicts(CFG, peaked=True))
+    m.model.eval()
+    dev = m.device
+    feats = [torch.from_numpy(O.features_from_fbank(fbank_for(b, t))).to(dev) for b, t in enumerate(FRAMES)]
+    lens = torch.tensor([f.shape[0] for f in feats])
+    from casr.vocab import load_vocab
+    i2w = load_vocab()[1]
+    g = m.eval_one_batch_with_greedy(dev, feats, lens, i2w, None)
+    assert g.pred_text == META["peaked"]["greedy"]["text"]
+    assert len(g.alignment) == META["peaked"]["greedy"]["steps"]
+    assert g.n == len(FRAMES)
+    r = m.eval_one_batch_with_beam(dev, 8, feats, lens, None, i2w, second_pass=False)
+    assert r.pred_text == META["peaked"]["beam8"]["text"]
+    assert r.alignment is None and r.text_len is None
+    with pytest.raises(AttributeError):  # reference: second_pass with lm_model None crashes
+        m.eval_one_batch_with_beam(dev, 4, feats, lens, None, i2w, second_pass=True, lm_model=None)
+    r = m.eval_one_batch_with_beam(dev, 4, feats, lens, None, pua_int2word(CFG.vocab), second_pass=True,
+                                   lm_model=StubLM(), lm_weight=1.5, length_weight=1.5)
+    assert [[ord(ch) - 0xE000 for ch in t] for t in r.pred_text] == META["peaked"]["beam4_lm"]["tokens"]
+
+
+def _bench_batch(eng, B, T=800):
+    x = np.stack([fbank_for(b, T) for b in range(B)])
+    fb = torch.from_numpy(x).to(eng.device)
+    return eng.features(fb, torch.full((B,), T, dtype=torch.int32, device=eng.device))
+
+
+def test_full_length_greedy_matches_oracle(eng):
+    """T = 800 (T' = 266), bench weights (no EOS: all 40 steps), B = 24 vs the CPU oracle."""
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True, eos_bias=0.0)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    B = 24
+    feat, flen = _bench_batch(eng, B)
+    eng.encode(feat, flen)
+    out = eng.greedy()
+    toks = out["tokens"].cpu().numpy()
+    feats = [O.features_from_fbank(fbank_for(b, 800)) for b in range(B)]
+    r = O.greedy_decode(feats, [266] * B, enc_sd, dec_sd)
+    np.testing.assert_array_equal(toks, r["all_tokens"])
+    np.testing.assert_allclose(out["accum"].cpu().numpy(), r["accum"], rtol=1e-5, atol=2e-3)
+
+
+def test_batch_invariance_and_determinism(eng):
+    """Size-independent properties at the benchmark size B = 256: two runs are bitwise equal,
+    and a 16-utterance sub-batch decodes to the same tokens as inside the full batch
+    (utterances are independent; the reference is batch-invariant too: SURVEY §8e)."""
+    eng.bind(pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True, eos_bias=0.0)))
+    feat, flen = _bench_batch(eng, 256)
+    eng.encode(feat, flen)
+    a = eng.greedy()["tokens"].cpu()
+    eng.encode(feat, flen)
+    b = eng.greedy()["tokens"].cpu()
+    assert torch.equal(a, b)
+    eng.encode(feat[100:116].contiguous(), flen[100:116].contiguous())
+    c = eng.greedy()["tokens"].cpu()
+    assert torch.equal(a[100:116], c)
+    eng.encode(feat[:64].contiguous(), flen[:64].contiguous())
+    r1 = eng.beam(8)
+    t1 = r1["tokens"].cpu()
+    eng.encode(feat[:16].contiguous(), flen[:16].contiguous())
+    t2 = eng.beam(8)["tokens"].cpu()
+    assert torch.equal(t1[:16], t2)

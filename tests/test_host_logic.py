@@ -1,0 +1,68 @@
+"""Host-side finalize rules (casr/results.py) against the reference semantics restated in the
+oracle and the reference-captured goldens: greedy score/length (model.py:582-593), loop
+length (model.py:578), finished-record ordering and second-pass selection (model.py:708-765)."""
+import numpy as np
+
+from golden_util import load_golden
+from casr.results import (edit_distance, get_wer, greedy_outputs, greedy_steps, records_by_utterance,
+                          second_pass_select)
+from stub_lm import StubLM, pua_int2word
+
+G, META = load_golden()
+
+
+def test_greedy_outputs_rules():
+    L = 6
+    tokens = np.array([[5, 6, 2, 7, 2, 2],     # EOS at step 2 -> len 2
+                       [2, 9, 9, 9, 9, 9],     # EOS at step 0 -> '' and 0.0
+                       [4, 4, 4, 4, 4, 4]])    # never finishes -> len L
+    out_len = np.array([2, 0, 6], np.int32)
+    fin = np.array([True, True, False])
+    accum = np.array([-3.0, -0.5, -12.0], np.float32)
+    toks, score = greedy_outputs(tokens, out_len, fin, accum)
+    assert toks == [[5, 6], [], [4] * 6]
+    assert score[0] == -3.0 / 3 and score[1] == 0.0 and score[2] == -12.0 / 6
+    assert greedy_steps(out_len, fin, L) == L
+    assert greedy_steps(np.array([2, 0]), np.array([True, True]), L) == 3
+
+
+def test_greedy_steps_match_golden():
+    for name in ("plain", "peaked"):
+        g = META[name]["greedy"]
+        lens = np.array(g["text_len"])
+        fin = lens < 40
+        assert greedy_steps(lens, fin, 40) == g["steps"]
+
+
+def test_records_order_and_first_max():
+    B, L, k = 2, 4, 3
+    rt = np.full((B, L, k, L), -1, np.int32)
+    rs = np.zeros((B, L, k), np.float32)
+    rv = np.zeros((B, L, k), np.uint8)
+    # utterance 0: step 1 rank 2 (score -1.0), step 0 rank 0 (score -1.0): equal scores, the
+    # earlier step must win (model.py:765 max keeps the first)
+    rv[0, 1, 2] = 1; rs[0, 1, 2] = -1.0; rt[0, 1, 2, :1] = [7]
+    rv[0, 0, 0] = 1; rs[0, 0, 0] = -1.0
+    rv[1, 3, 1] = 1; rs[1, 3, 1] = -2.5; rt[1, 3, 1, :3] = [4, 5, 6]
+    recs = records_by_utterance(rt, rs, rv)
+    assert recs[0] == [([], -1.0), ([7], -1.0)]
+    assert recs[1] == [([4, 5, 6], -2.5)]
+    best = {b: max(v, key=lambda e: e[1]) for b, v in recs.items()}
+    assert best[0] == ([], -1.0)
+
+
+def test_second_pass_rule():
+    i2w = pua_int2word(5004)
+    lm = StubLM()
+    recs = {0: [([10, 11], -3.0), ([10], -2.0), ([10, 11, 12, 13], -3.5)], 1: [([4], -9.0)]}
+    sel = second_pass_select(recs, i2w, lm, 1.5, 1.5)
+    comb = [s + 1.5 * lm.score(" ".join(i2w[i] for i in t), bos=True) + 1.5 * len(t) for t, s in recs[0]]
+    assert sel[0] == recs[0][int(np.argmax(comb))]
+    assert sel[1] == recs[1][0]  # a single finished hypothesis is taken as is
+
+
+def test_wer():
+    assert edit_distance("abc", "abc") == 0
+    assert edit_distance("", "abc") == 3
+    assert edit_distance("kitten", "sitting") == 3
+    assert get_wer("ab", "abcd") == 0.5
