@@ -155,6 +155,7 @@ def main():
 
     for _ in range(args.warmup):
         step_greedy()
+    flags = eng.device_flags()  # decode guard bits: 0 = every index stayed in range
     # one instrumented step: per-class launch times -> dominant kernel
     eng.profile(["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"])
     step_greedy()
@@ -223,6 +224,7 @@ def main():
                          "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s},
             "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},
             "weights_bcast_s": weight_s,
+            "device_flags": flags,
             "cpu_baseline": cpu,
         }
         if cpu:

@@ -138,6 +138,16 @@ class Engine:
         _lib.check(self.lib.casr_beam_records(self.handle, _ptr(rt), _ptr(rs), _ptr(rv), _stream()), self.handle)
         return rt, rs, rv
 
+    def device_flags(self):
+        """Guard bits of the last decode (0 = clean); synchronises the stream."""
+        f = ctypes.c_int32()
+        _lib.check(self.lib.casr_device_flags(self.handle, ctypes.byref(f), _stream()), self.handle)
+        return f.value
+
+    def set_graphs(self, enable):
+        """hipGraph replay of the launch-bound loops (default on); off = eager launches."""
+        _lib.check(self.lib.casr_set_graphs(self.handle, int(bool(enable))), self.handle)
+
     # ------------------------------------------------------------------ launch timing
     def profile(self, classes):
         """Enable HIP-event timing for the named kernel classes (lib.KERNEL_CLASSES)."""

@@ -1,0 +1,278 @@
+// Bahdanau additive attention of one decode step on gfx950 (BauAttn.forward, heads == 1,
+// attention.py:80-95):
+//   q[r]    = h[r] . W_hidden                        (torch.mm, attention.py:92)
+//   e[r][t] = sum_a v[a] * tanh(keys[b][t][a] + q[r][a])
+//   alpha   = softmax_t(mask + e),   ctx[r] = sum_t alpha[r][t] * enc[b][t]   (:93-95)
+// for every decoder row r = b*k + j.  Keys/values are per utterance (the reference tiles
+// and re-gathers them per beam, model.py:660-669 / :913-916): a block serves up to KPB
+// beam rows of one utterance, so each utterance's keys and values are streamed
+// ceil(k / KPB) times per step instead of k times.
+//
+// HBM/L2-bound streaming + transcendental work, no MFMA.  512 threads: every phase has
+// 8 waves with several 16 B loads in flight per lane; partial sums are combined through
+// LDS in a fixed order (results are deterministic).  keysT is [B][A][Tq] (Tq = Tp rounded
+// up to 4) so a lane reads 4 consecutive time steps of one key row.
+#include "casr_common.h"
+#include "casr_internal.h"
+
+namespace casr {
+
+constexpr int AT_THREADS = 512;
+constexpr int AT_WAVES = AT_THREADS / 64;
+
+__host__ __device__ constexpr int attn_tq(int Tp) { return (Tp + 3) & ~3; }
+
+template <int KPB>
+__host__ __device__ constexpr int attn_scratch_floats(int Tq) {
+  // q partials [16][KPB][A] | score partials [8][KPB][Tq] | context partials [4][KPB][C]
+  return (16 * KPB * A > AT_WAVES * KPB * Tq)
+             ? (16 * KPB * A > 4 * KPB * C ? 16 * KPB * A : 4 * KPB * C)
+             : (AT_WAVES * KPB * Tq > 4 * KPB * C ? AT_WAVES * KPB * Tq : 4 * KPB * C);
+}
+
+template <int KPB>
+__host__ __device__ constexpr size_t attn_smem_floats(int Tp) {
+  return (size_t)KPB * HD + KPB * A + A + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp);
+}
+
+// tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|), on v_exp_f32 / v_rcp_f32.  Absolute
+// error <= ~3e-7: every term of the score sum is this times |v[a]| (~0.1) and 128 terms are
+// summed, so the scores stay within ~1e-6 of the libm form (tests: alignment within 1e-5).
+CASR_DEV float tanh_fast(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  return copysignf(__fdividef(1.f - e, 1.f + e), x);
+}
+
+template <int KPB>
+__global__ __launch_bounds__(AT_THREADS) void attention_kernel(
+    float* __restrict__ st, const float* __restrict__ keysT, const float* __restrict__ enc,
+    const int32_t* __restrict__ lens, const float* __restrict__ Wh, const float* __restrict__ vv,
+    int k, int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l, int total) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ float wred[2][AT_WAVES][KPB];
+  if (done_before(newdone, l) >= total) return;
+  const int Tq = attn_tq(Tp);
+  float* hs = sm;                  // [KPB][HD]
+  float* qs = hs + KPB * HD;       // [KPB][A]
+  float* vs = qs + KPB * A;        // [A]
+  float* xs = vs + A;              // scratch
+  float* es = xs + attn_scratch_floats<KPB>(Tq);  // [KPB][Tq]
+  const int b = blockIdx.x, j0 = blockIdx.y * KPB;
+  const int nk = min(KPB, k - j0);
+  const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
+  const int len = min(lens[b], Tp);
+  const size_t row0 = (size_t)b * k + j0;
+
+  // 1. h rows and v -> LDS
+  for (int i = tid; i < nk * (HD / 4); i += AT_THREADS) {
+    const int j = i / (HD / 4), c4 = i - j * (HD / 4);
+    reinterpret_cast<float4*>(hs + j * HD)[c4] = reinterpret_cast<const float4*>(st + (row0 + j) * ST + C)[c4];
+  }
+  if (tid < A) vs[tid] = vv[tid];
+  __syncthreads();
+
+  // 2. q = h . W_hidden: thread = 4 columns x 32 of the 512 rows; 16 partials per column
+  {
+    const int a4 = tid & 31, p = tid >> 5;
+    float acc[KPB][4];
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) acc[j][0] = acc[j][1] = acc[j][2] = acc[j][3] = 0.f;
+    const float* wp = Wh + (size_t)(p * 32) * A + 4 * a4;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) {
+      const float4 w4 = *reinterpret_cast<const float4*>(wp + (size_t)i * A);
+#pragma unroll
+      for (int j = 0; j < KPB; ++j) {
+        const float hv = hs[j * HD + p * 32 + i];
+        acc[j][0] = fmaf(hv, w4.x, acc[j][0]);
+        acc[j][1] = fmaf(hv, w4.y, acc[j][1]);
+        acc[j][2] = fmaf(hv, w4.z, acc[j][2]);
+        acc[j][3] = fmaf(hv, w4.w, acc[j][3]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KPB; ++j)
+      if (j < nk)
+        *reinterpret_cast<float4*>(xs + (p * KPB + j) * A + 4 * a4) =
+            make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+  }
+  __syncthreads();
+  for (int i = tid; i < nk * A; i += AT_THREADS) {
+    const int j = i / A, a = i - j * A;
+    float q = 0.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) q += xs[(p * KPB + j) * A + a];
+    qs[j * A + a] = q;
+  }
+  __syncthreads();
+
+  // 3. scores: wave w owns a in [16w, 16w + 16); lane owns 4 consecutive t
+  const float* kb = keysT + (size_t)b * A * Tq;
+  for (int t0 = 4 * ln; t0 < Tq; t0 += 256) {
+    float e4[KPB][4];
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) e4[j][0] = e4[j][1] = e4[j][2] = e4[j][3] = 0.f;
+    if (t0 < len) {
+#pragma unroll 4
+      for (int ai = 0; ai < A / AT_WAVES; ++ai) {
+        const int a = wv * (A / AT_WAVES) + ai;
+        const float4 kv = *reinterpret_cast<const float4*>(kb + (size_t)a * Tq + t0);
+        const float va = vs[a];
+#pragma unroll
+        for (int j = 0; j < KPB; ++j)
+          if (j < nk) {
+            const float qa = qs[j * A + a];
+            e4[j][0] = __fadd_rn(e4[j][0], __fmul_rn(tanh_fast(kv.x + qa), va));
+            e4[j][1] = __fadd_rn(e4[j][1], __fmul_rn(tanh_fast(kv.y + qa), va));
+            e4[j][2] = __fadd_rn(e4[j][2], __fmul_rn(tanh_fast(kv.z + qa), va));
+            e4[j][3] = __fadd_rn(e4[j][3], __fmul_rn(tanh_fast(kv.w + qa), va));
+          }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KPB; ++j)
+      if (j < nk)
+        *reinterpret_cast<float4*>(xs + (wv * KPB + j) * Tq + t0) =
+            make_float4(e4[j][0], e4[j][1], e4[j][2], e4[j][3]);
+  }
+  __syncthreads();
+
+  // combine the 8 wave partials (fixed order), mask past len, row maxima
+  float lmax[KPB];
+#pragma unroll
+  for (int j = 0; j < KPB; ++j) {
+    lmax[j] = -INFINITY;
+    if (j < nk)
+      for (int t = tid; t < Tq; t += AT_THREADS) {
+        float ev = -INFINITY;
+        if (t < len) {
+          const float* x = xs + j * Tq + t;
+          const int ws = KPB * Tq;
+          ev = ((x[0] + x[ws]) + (x[2 * ws] + x[3 * ws])) + ((x[4 * ws] + x[5 * ws]) + (x[6 * ws] + x[7 * ws]));
+        }
+        es[j * Tq + t] = ev;
+        lmax[j] = fmaxf(lmax[j], ev);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < KPB; ++j)
+    if (j < nk) {
+      const float m = wave_max(lmax[j]);
+      if (ln == 0) wred[0][wv][j] = m;
+    }
+  __syncthreads();
+  float rmax[KPB], lsum[KPB];
+#pragma unroll
+  for (int j = 0; j < KPB; ++j) {
+    float m = -INFINITY;
+    if (j < nk)
+#pragma unroll
+      for (int w = 0; w < AT_WAVES; ++w) m = fmaxf(m, wred[0][w][j]);
+    rmax[j] = m;
+    lsum[j] = 0.f;
+  }
+  // 4. softmax over t (torch: exp(x - max), sum, then * 1/sum)
+#pragma unroll
+  for (int j = 0; j < KPB; ++j)
+    if (j < nk)
+      for (int t = tid; t < Tq; t += AT_THREADS) {
+        const float p = expf(es[j * Tq + t] - rmax[j]);
+        es[j * Tq + t] = p;
+        lsum[j] += p;
+      }
+#pragma unroll
+  for (int j = 0; j < KPB; ++j)
+    if (j < nk) {
+      const float s = wave_sum(lsum[j]);
+      if (ln == 0) wred[1][wv][j] = s;
+    }
+  __syncthreads();
+  float rinv[KPB];
+#pragma unroll
+  for (int j = 0; j < KPB; ++j) {
+    float s = 0.f;
+    if (j < nk)
+      s = ((wred[1][0][j] + wred[1][1][j]) + (wred[1][2][j] + wred[1][3][j])) +
+          ((wred[1][4][j] + wred[1][5][j]) + (wred[1][6][j] + wred[1][7][j]));
+    rinv[j] = 1.0f / s;
+  }
+  const size_t R = (size_t)gridDim.x * k;
+#pragma unroll
+  for (int j = 0; j < KPB; ++j)
+    if (j < nk)
+      for (int t = tid; t < Tq; t += AT_THREADS) {
+        const float al = es[j * Tq + t] * rinv[j];
+        es[j * Tq + t] = al;
+        if (align && t < Tp) align[(size_t)t * R + row0 + j] = al;
+      }
+  __syncthreads();
+
+  // 5. context: thread = 4 columns x every 4th t (4 partials, combined in a fixed order)
+  {
+    const int c4 = tid & 127, tp = tid >> 7;
+    float acc[KPB][4];
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) acc[j][0] = acc[j][1] = acc[j][2] = acc[j][3] = 0.f;
+    const float* eb = enc + (size_t)b * Tp * C + 4 * c4;
+#pragma unroll 8
+    for (int t = tp; t < len; t += 4) {
+      const float4 v4 = *reinterpret_cast<const float4*>(eb + (size_t)t * C);
+#pragma unroll
+      for (int j = 0; j < KPB; ++j)
+        if (j < nk) {
+          const float al = es[j * Tq + t];
+          acc[j][0] = __fadd_rn(acc[j][0], __fmul_rn(al, v4.x));
+          acc[j][1] = __fadd_rn(acc[j][1], __fmul_rn(al, v4.y));
+          acc[j][2] = __fadd_rn(acc[j][2], __fmul_rn(al, v4.z));
+          acc[j][3] = __fadd_rn(acc[j][3], __fmul_rn(al, v4.w));
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < KPB; ++j)
+      if (j < nk)
+        *reinterpret_cast<float4*>(xs + (tp * KPB + j) * C + 4 * c4) =
+            make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
+  }
+  __syncthreads();
+  for (int i = tid; i < nk * (C / 4); i += AT_THREADS) {
+    const int j = i / (C / 4), c4 = i - j * (C / 4);
+    const float4 p0 = *reinterpret_cast<const float4*>(xs + (0 * KPB + j) * C + 4 * c4);
+    const float4 p1 = *reinterpret_cast<const float4*>(xs + (1 * KPB + j) * C + 4 * c4);
+    const float4 p2 = *reinterpret_cast<const float4*>(xs + (2 * KPB + j) * C + 4 * c4);
+    const float4 p3 = *reinterpret_cast<const float4*>(xs + (3 * KPB + j) * C + 4 * c4);
+    *reinterpret_cast<float4*>(st + (row0 + j) * ST + 4 * c4) =
+        make_float4((p0.x + p1.x) + (p2.x + p3.x), (p0.y + p1.y) + (p2.y + p3.y),
+                    (p0.z + p1.z) + (p2.z + p3.z), (p0.w + p1.w) + (p2.w + p3.w));
+  }
+}
+
+template <int KPB>
+static hipError_t launch_kpb(const DecodeArgs& a, float* st, float* align, int32_t* newdone, int l,
+                             int total, hipStream_t s) {
+  const size_t shm = attn_smem_floats<KPB>(a.Tp) * sizeof(float);
+  static size_t raised = 0;  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950)
+  if (shm > raised) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(attention_kernel<KPB>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+    raised = shm;
+  }
+  dim3 grid(a.B, (a.k + KPB - 1) / KPB);
+  hipLaunchKernelGGL(attention_kernel<KPB>, grid, dim3(AT_THREADS), shm, s, st, a.keysT, a.enc, a.lens,
+                     a.W + a.L.w_hidden, a.W + a.L.v, a.k, a.Tp, align, newdone, l, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_attention_step(const DecodeArgs& a, float* st, float* align, int32_t* newdone,
+                                 int l, int total, hipStream_t s) {
+  if (a.k == 1) return launch_kpb<1>(a, st, align, newdone, l, total, s);
+  if (a.k == 2) return launch_kpb<2>(a, st, align, newdone, l, total, s);
+  return launch_kpb<4>(a, st, align, newdone, l, total, s);
+}
+
+size_t attention_smem_bytes(int k, int Tp) {
+  const size_t f = k == 1 ? attn_smem_floats<1>(Tp) : k == 2 ? attn_smem_floats<2>(Tp) : attn_smem_floats<4>(Tp);
+  return f * sizeof(float);
+}
+
+}  // namespace casr

@@ -108,10 +108,71 @@ struct casr_handle {
   // decoder workspace
   DevBuf st, logits, small, bp, tk, rec, beam_small;
   DecodeBufs d{};
+  DevBuf gout;  // internal decode outputs written by captured graphs
   Profiler prof;
   int dec_k = 0;
   bool beam_done = false;
+  // hipGraph replay of the launch-bound loops (per-layer recurrence, decode loop)
+  bool use_graphs = true;
+  hipStream_t cap = nullptr;      // capture stream
+  hipStream_t xs[2] = {};         // replay streams, fenced to the caller's stream by events
+  hipEvent_t ev_in = nullptr, ev_out[2] = {};
+  GraphCache graphs;
 };
+
+static int fail(casr_handle* h, int code, const char* fmt, ...);
+
+// Capture `body(stream)` once per key into a hipGraph on the handle's private capture stream,
+// then replay it on the private replay stream, ordered after everything already enqueued on
+// the caller's stream and before anything enqueued there afterwards (event fences both
+// ways; the caller's stream may be the legacy null stream, which a graph is not launched on).
+template <class Body>
+static hipError_t get_graph(casr_handle* h, const std::vector<uint64_t>& key, Body&& body,
+                            hipGraphExec_t* out) {
+  hipError_t e;
+  if (!h->cap) {
+    e = hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&h->xs[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&h->ev_out[i], hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  hipGraphExec_t exec = h->graphs.find(key);
+  if (!exec) {
+    e = hipStreamBeginCapture(h->cap, hipStreamCaptureModeRelaxed);
+    if (e != hipSuccess) return e;
+    hipError_t eb = body(h->cap);
+    hipGraph_t g = nullptr;
+    e = hipStreamEndCapture(h->cap, &g);
+    if (eb != hipSuccess) e = eb;
+    if (e == hipSuccess) e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    if (e != hipSuccess) return e;
+    h->graphs.add(key, exec);
+  }
+  *out = exec;
+  return hipSuccess;
+}
+
+// Replay n (<= 2) graphs concurrently, graph i on replay stream i, all after the work already
+// on `s` and before anything enqueued on `s` afterwards.
+static hipError_t launch_graphs(casr_handle* h, const hipGraphExec_t* ex, int n, hipStream_t s) {
+  hipError_t e = hipEventRecord(h->ev_in, s);
+  for (int i = 0; i < n && e == hipSuccess; ++i) {
+    e = hipStreamWaitEvent(h->xs[i], h->ev_in, 0);
+    if (e == hipSuccess) e = hipGraphLaunch(ex[i], h->xs[i]);
+    if (e == hipSuccess) e = hipEventRecord(h->ev_out[i], h->xs[i]);
+  }
+  for (int i = 0; i < n && e == hipSuccess; ++i) e = hipStreamWaitEvent(s, h->ev_out[i], 0);
+  return e;
+}
+
+template <class Body>
+static hipError_t run_graph(casr_handle* h, const std::vector<uint64_t>& key, hipStream_t s, Body&& body) {
+  hipGraphExec_t exec = nullptr;
+  hipError_t e = get_graph(h, key, body, &exec);
+  return e == hipSuccess ? launch_graphs(h, &exec, 1, s) : e;
+}
 
 static int fail(casr_handle* h, int code, const char* fmt, ...) {
   char buf[512];
@@ -246,10 +307,23 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
 void casr_destroy(casr_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
+  h->graphs.clear();
+  if (h->cap) (void)hipStreamDestroy(h->cap);
+  for (int i = 0; i < 2; ++i) {
+    if (h->xs[i]) (void)hipStreamDestroy(h->xs[i]);
+    if (h->ev_out[i]) (void)hipEventDestroy(h->ev_out[i]);
+  }
+  if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens,
-                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small})
+                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout})
     b->release();
   delete h;
+}
+
+int casr_set_graphs(casr_handle* h, int enable) {
+  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
+  h->use_graphs = enable != 0;
+  return CASR_OK;
 }
 
 const char* casr_last_error(const casr_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
@@ -286,7 +360,8 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   HIP_OK(h, h->hbuf.ensure((size_t)2 * 2 * B * H * sizeof(float)));
   HIP_OK(h, h->cst.ensure((size_t)2 * B * H * sizeof(float)));
   HIP_OK(h, h->hfin.ensure((size_t)2 * B * H * sizeof(float)));
-  HIP_OK(h, h->keysT.ensure(rows * A * sizeof(float)));
+  const int Tq = (Tp + 3) & ~3;  // keysT row stride (16 B aligned rows for the attention)
+  HIP_OK(h, h->keysT.ensure((size_t)B * A * Tq * sizeof(float)));
   HIP_OK(h, h->lens.ensure((size_t)B * sizeof(int32_t)));
   HIP_OK(h, hipMemcpyAsync(h->lens.p, lens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
   HIP_OK(h, hipMemsetAsync(h->out0.p, 0, rows * C * sizeof(float), s));
@@ -304,15 +379,43 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
     HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
                                 h->gin.as<float>(), s));
     }
-    HIP_OK(h, hipMemsetAsync(hb, 0, (size_t)2 * B * H * sizeof(float), s));
-    HIP_OK(h, hipMemsetAsync(h->cst.p, 0, (size_t)2 * B * H * sizeof(float), s));
     const int residual = (h->cfg.residual && l > 0) ? 1 : 0;
-    for (int step = 0; step < Tp; ++step) {
-      const float* hprev = hb + (size_t)(step & 1) * 2 * B * H;
-      float* hnext = hb + (size_t)((step + 1) & 1) * 2 * B * H;
-      ProfScope ps(&h->prof, CASR_K_REC_STEP, s);
-      HIP_OK(h, launch_rec_step(h->W + h->L.enc_whh[l], h->gin.as<float>(), x, out, hprev, hnext,
-                                h->cst.as<float>(), h->hfin.as<float>(), dl, B, Tp, step, residual, s));
+    // layer 0 has no residual input: pass an internal pointer so a graph never bakes in the
+    // caller's feature buffer
+    const float* xin = residual ? x : out;
+    // h (both ping-pong buffers) and c start at zero (RNN_RES state None, util.py:1236-1247)
+    HIP_OK(h, fill_u32(hb, 0, (size_t)2 * 2 * B * H, s));
+    HIP_OK(h, fill_u32(h->cst.p, 0, (size_t)2 * B * H, s));
+    auto rec_loop = [&](hipStream_t st, Profiler* prof, int r0, int r1) -> hipError_t {
+      hipError_t e = hipSuccess;
+      for (int step = 0; step < Tp && e == hipSuccess; ++step) {
+        const float* hprev = hb + (size_t)(step & 1) * 2 * B * H;
+        float* hnext = hb + (size_t)((step + 1) & 1) * 2 * B * H;
+        ProfScope ps(prof, CASR_K_REC_STEP, st);
+        e = launch_rec_step(h->W + h->L.enc_whh[l], h->gin.as<float>(), xin, out, hprev, hnext,
+                            h->cst.as<float>(), h->hfin.as<float>(), dl, B, Tp, step, residual, r0, r1, st);
+      }
+      return e;
+    };
+    if (h->use_graphs) {
+      // rows are independent: two row halves replay as two graphs on two streams, so one
+      // half's load latency hides behind the other's MFMAs
+      const int nsplit = B >= 64 ? 2 : 1;
+      const int half = ((B / 2) + 15) / 16 * 16;
+      hipGraphExec_t ex[2] = {};
+      for (int p = 0; p < nsplit; ++p) {
+        const int r0 = (nsplit == 1 || p == 0) ? 0 : half;
+        const int r1 = (nsplit == 1 || p == 1) ? B : half;
+        const std::vector<uint64_t> key = {1, (uint64_t)l, (uint64_t)B, (uint64_t)Tp, (uint64_t)residual,
+                                           (uint64_t)r0, (uint64_t)r1, (uint64_t)h->W, (uint64_t)h->gin.p,
+                                           (uint64_t)xin, (uint64_t)out, (uint64_t)hb, (uint64_t)h->cst.p,
+                                           (uint64_t)h->hfin.p, (uint64_t)dl};
+        HIP_OK(h, get_graph(h, key, [&](hipStream_t cs) { return rec_loop(cs, nullptr, r0, r1); }, &ex[p]));
+      }
+      ProfScope ps(&h->prof, CASR_K_REC_STEP, s, Tp);  // one pair per replay of Tp steps
+      HIP_OK(h, launch_graphs(h, ex, nsplit, s));
+    } else {
+      HIP_OK(h, rec_loop(s, &h->prof, 0, B));
     }
     x = out;
   }
@@ -350,8 +453,16 @@ int casr_encoder_results(casr_handle* h, float* enc, float* h_final, float* c_fi
     HIP_OK(h, hipMemcpy2DAsync(c_final + H, C * sizeof(float), h->cst.as<float>() + (size_t)B * H,
                                H * sizeof(float), H * sizeof(float), B, hipMemcpyDeviceToDevice, s));
   if (keys)
-    HIP_OK(h, hipMemcpyAsync(keys, h->keysT.p, (size_t)B * Tp * A * sizeof(float), hipMemcpyDeviceToDevice, s));
+    HIP_OK(h, hipMemcpy2DAsync(keys, Tp * sizeof(float), h->keysT.p, ((Tp + 3) & ~3) * sizeof(float),
+                               Tp * sizeof(float), (size_t)B * A, hipMemcpyDeviceToDevice, s));
   return CASR_OK;
+}
+
+// the decode loop replays as a graph unless a decode kernel class is being timed per launch
+static bool decode_graph_ok(const casr_handle* h) {
+  const uint32_t dec = (1u << CASR_K_DEC_LSTM) | (1u << CASR_K_ATTENTION) | (1u << CASR_K_PROJ) |
+                       (1u << CASR_K_SELECT);
+  return h->use_graphs && !(h->prof.mask & dec);
 }
 
 static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
@@ -364,7 +475,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
     return fail(h, CASR_ERR_UNSUPPORTED, "attention needs %zu B of LDS (k=%d, Tp=%d) > 160 KiB", smem, k, Tp);
   HIP_OK(h, h->st.ensure((size_t)2 * R * ST * sizeof(float)));
   HIP_OK(h, h->logits.ensure((size_t)R * V * sizeof(float)));
-  HIP_OK(h, h->small.ensure((size_t)(6 * R + L + B + R) * sizeof(int32_t) + 256));
+  HIP_OK(h, h->small.ensure((size_t)(6 * R + L + B + R + 1) * sizeof(int32_t) + 256));
   HIP_OK(h, h->bp.ensure((size_t)L * R * sizeof(int32_t)));
   HIP_OK(h, h->tk.ensure((size_t)L * R * sizeof(int32_t)));
   HIP_OK(h, h->rec.ensure((size_t)B * L * k * (sizeof(float) + sizeof(int32_t) + 1) + 256));
@@ -382,6 +493,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   d.newdone = sp + 6 * R;
   d.topfin = reinterpret_cast<uint8_t*>(sp + 6 * R + L);
   d.fin = reinterpret_cast<uint8_t*>(sp + 6 * R + L + B);
+  d.err = sp + 6 * R + L + B + R;
   d.bp = h->bp.as<int32_t>();
   d.tk = h->tk.as<int32_t>();
   d.rec_score = h->rec.as<float>();
@@ -413,7 +525,31 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   DecodeArgs a{};
   int rc = prepare_decode(h, 1, a);
   if (rc) return rc;
-  HIP_OK(h, run_greedy(a, h->d, tokens, out_len, finished, accum, align, (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
+  if (!decode_graph_ok(h)) {
+    HIP_OK(h, run_greedy(a, h->d, tokens, out_len, finished, accum, align, s));
+    return CASR_OK;
+  }
+  // graph replay into handle-owned outputs, then copies to the caller's buffers
+  const int B = h->B, L = h->cfg.max_len;
+  const size_t nal = align ? (size_t)L * h->Tp * B : 0;
+  HIP_OK(h, h->gout.ensure(sizeof(int32_t) * ((size_t)B * L + B) + sizeof(float) * (B + nal) + B + 64));
+  int32_t* itok = h->gout.as<int32_t>();
+  int32_t* ilen = itok + (size_t)B * L;
+  float* iacc = reinterpret_cast<float*>(ilen + B);
+  float* ial = align ? iacc + B : nullptr;
+  uint8_t* ifin = reinterpret_cast<uint8_t*>(iacc + B + nal);
+  a.prof = nullptr;
+  const std::vector<uint64_t> key = {2, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
+                                     (uint64_t)(align != nullptr), (uint64_t)h->st.p, (uint64_t)h->logits.p,
+                                     (uint64_t)h->small.p, (uint64_t)h->enc_out, (uint64_t)h->keysT.p,
+                                     (uint64_t)h->hfin.p, (uint64_t)h->cst.p, (uint64_t)h->lens.p};
+  HIP_OK(h, run_graph(h, key, s, [&](hipStream_t cs) { return run_greedy(a, h->d, itok, ilen, ifin, iacc, ial, cs); }));
+  HIP_OK(h, hipMemcpyAsync(tokens, itok, sizeof(int32_t) * B * L, hipMemcpyDeviceToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(out_len, ilen, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(finished, ifin, B, hipMemcpyDeviceToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(accum, iacc, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
+  if (align) HIP_OK(h, hipMemcpyAsync(align, ial, sizeof(float) * nal, hipMemcpyDeviceToDevice, s));
   return CASR_OK;
 }
 
@@ -425,10 +561,35 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
   DecodeArgs a{};
   int rc = prepare_decode(h, k, a);
   if (rc) return rc;
-  HIP_OK(h, run_beam(a, h->d, lm_weight, length_weight, best_tokens, best_len, best_score, steps,
-                     (hipStream_t)stream));
+  hipStream_t s = (hipStream_t)stream;
   h->dec_k = k;
   h->beam_done = true;
+  if (!decode_graph_ok(h)) {
+    HIP_OK(h, run_beam(a, h->d, lm_weight, length_weight, best_tokens, best_len, best_score, steps, s));
+    return CASR_OK;
+  }
+  const int B = h->B, L = h->cfg.max_len;
+  HIP_OK(h, h->gout.ensure(sizeof(int32_t) * ((size_t)B * L + B + 1) + sizeof(float) * B + 64));
+  int32_t* itok = h->gout.as<int32_t>();
+  int32_t* ilen = itok + (size_t)B * L;
+  int32_t* istp = ilen + B;
+  float* isc = reinterpret_cast<float*>(istp + 1);
+  a.prof = nullptr;
+  uint32_t lmw, lw;
+  std::memcpy(&lmw, &lm_weight, 4);
+  std::memcpy(&lw, &length_weight, 4);
+  const std::vector<uint64_t> key = {3, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
+                                     (uint64_t)h->gout.p, (uint64_t)h->st.p, (uint64_t)h->logits.p,
+                                     (uint64_t)h->small.p, (uint64_t)h->bp.p, (uint64_t)h->tk.p, (uint64_t)h->rec.p,
+                                     (uint64_t)h->enc_out, (uint64_t)h->keysT.p, (uint64_t)h->hfin.p,
+                                     (uint64_t)h->cst.p, (uint64_t)h->lens.p};
+  HIP_OK(h, run_graph(h, key, s, [&](hipStream_t cs) {
+    return run_beam(a, h->d, lm_weight, length_weight, itok, ilen, isc, istp, cs);
+  }));
+  HIP_OK(h, hipMemcpyAsync(best_tokens, itok, sizeof(int32_t) * B * L, hipMemcpyDeviceToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(best_len, ilen, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(best_score, isc, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
+  HIP_OK(h, hipMemcpyAsync(steps, istp, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
   return CASR_OK;
 }
 
@@ -441,6 +602,17 @@ int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uin
   int rc = prepare_decode(h, h->dec_k, a);
   if (rc) return rc;
   HIP_OK(h, run_beam_records(a, h->d, rec_tokens, rec_score, rec_valid, (hipStream_t)stream));
+  return CASR_OK;
+}
+
+int casr_device_flags(casr_handle* h, int32_t* flags, void* stream) {
+  if (!h || !flags) return fail(h, CASR_ERR_ARG, "casr_device_flags: bad arguments");
+  *flags = 0;
+  if (!h->d.err) return CASR_OK;
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  HIP_OK(h, hipMemcpyAsync(flags, h->d.err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_OK(h, hipStreamSynchronize(s));
   return CASR_OK;
 }
 
@@ -457,13 +629,15 @@ int casr_profile_read(casr_handle* h, int cls, int32_t* launches, double* total_
   Profiler& p = h->prof;
   const size_t n = p.used[cls] / 2;
   double ms = 0.0;
+  int32_t nl = 0;
   if (n) HIP_OK(h, hipEventSynchronize(p.ev[cls][2 * n - 1]));
   for (size_t i = 0; i < n; ++i) {
     float t = 0.f;
     HIP_OK(h, hipEventElapsedTime(&t, p.ev[cls][2 * i], p.ev[cls][2 * i + 1]));
     ms += t;
+    nl += p.weight[cls][i];
   }
-  *launches = (int32_t)n;
+  *launches = nl;
   *total_ms = ms;
   return CASR_OK;
 }

@@ -19,6 +19,14 @@ CASR_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 // expf/tanhf; the fast __expf differs by a few ulp, so it is not used for gates).
 CASR_DEV float sigmoid_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Decode early exit (model.py:578, :897-901): newdone[s] counts rows / utterances that
+// finished at step s; step l runs only while fewer than `total` finished before it.
+CASR_DEV int done_before(const int32_t* __restrict__ newdone, int l) {
+  int s = 0;
+  for (int i = 0; i < l; ++i) s += newdone[i];
+  return s;
+}
+
 CASR_DEV float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -24,6 +24,14 @@ constexpr int KPROJ = C + HD;     // 1024: projection contraction [ctx | h]
 constexpr int ST = C + HD + HD;   // 1536: per-row decoder state [ctx | h | c]
 constexpr int KMAX_BEAM = 16;
 
+// Device guard bits: a data-dependent index (token id, predecessor row, back-pointer) out of
+// range is clamped to a valid one and reported here instead of faulting the GPU.
+constexpr int CASR_DEV_BAD_TOKEN = 1;    // decoder input token not in [0, V)
+constexpr int CASR_DEV_BAD_SRC = 2;      // predecessor row not in [0, R)
+constexpr int CASR_DEV_NAN_LOGITS = 4;   // no finite maximum in a logit row (greedy)
+constexpr int CASR_DEV_BAD_CAND = 8;     // beam candidate index not in [0, k*V)
+constexpr int CASR_DEV_BAD_BACKPTR = 16; // back-pointer walk left [0, k)
+
 // MFMA-fragment-major weight block: a 16-row x 64-k tile stored as [q=0..3][lane][4] so
 // lane l reads row (l&15), k = 16*(l>>4) + 4q + e with one coalesced 16 B load per q.
 constexpr int FRAG = 16 * 64;
@@ -57,13 +65,20 @@ inline int packed_gate_row(int g, int u) { return (u / 16) * 64 + g * 16 + (u % 
 struct Profiler {
   uint32_t mask = 0;
   std::vector<hipEvent_t> ev[CASR_K_COUNT];
+  std::vector<int> weight[CASR_K_COUNT];  // launches covered by each event pair
   size_t used[CASR_K_COUNT] = {};
-  void mark(int cls, hipStream_t s) {
-    if (!((mask >> cls) & 1u)) return;
+  bool on(int cls) const { return (mask >> cls) & 1u; }
+  // n > 1: the pair brackets a graph replay of n launches of this class (boundaries included)
+  void mark(int cls, hipStream_t s, int n = 1) {
+    if (!on(cls)) return;
     if (used[cls] == ev[cls].size()) {
       hipEvent_t e;
       if (hipEventCreate(&e) != hipSuccess) return;
       ev[cls].push_back(e);
+    }
+    if ((used[cls] & 1) == 0) {
+      if (weight[cls].size() <= used[cls] / 2) weight[cls].resize(used[cls] / 2 + 1);
+      weight[cls][used[cls] / 2] = n;
     }
     (void)hipEventRecord(ev[cls][used[cls]++], s);
   }
@@ -81,15 +96,50 @@ struct ProfScope {
   Profiler* p;
   int cls;
   hipStream_t s;
-  ProfScope(Profiler* p_, int c, hipStream_t s_) : p(p_), cls(c), s(s_) {
-    if (p) p->mark(cls, s);
+  ProfScope(Profiler* p_, int c, hipStream_t s_, int n = 1) : p(p_), cls(c), s(s_) {
+    if (p) p->mark(cls, s, n);
   }
   ~ProfScope() {
     if (p) p->mark(cls, s);
   }
 };
 
+// Instantiated hipGraphs keyed by everything a captured sequence bakes in (shapes, weight
+// and workspace pointers, scalar arguments).  A key miss re-captures; a small LRU bound
+// keeps stale entries (e.g. after a workspace grew) from piling up.
+struct GraphCache {
+  struct Entry {
+    std::vector<uint64_t> key;
+    hipGraphExec_t exec;
+  };
+  std::vector<Entry> entries;
+  hipGraphExec_t find(const std::vector<uint64_t>& key) {
+    for (size_t i = 0; i < entries.size(); ++i)
+      if (entries[i].key == key) {
+        if (i + 1 != entries.size()) std::swap(entries[i], entries.back());
+        return entries.back().exec;
+      }
+    return nullptr;
+  }
+  void add(std::vector<uint64_t> key, hipGraphExec_t exec) {
+    if (entries.size() >= 24) {
+      (void)hipGraphExecDestroy(entries.front().exec);
+      entries.erase(entries.begin());
+    }
+    entries.push_back(Entry{std::move(key), exec});
+  }
+  void clear() {
+    for (auto& e : entries) (void)hipGraphExecDestroy(e.exec);
+    entries.clear();
+  }
+  ~GraphCache() { clear(); }
+};
+
 // ---------------------------------------------------------------- kernel launchers
+// fill.hip (graph-safe replacements for hipMemsetAsync)
+hipError_t fill_u32(void* p, uint32_t v, size_t n_words, hipStream_t s);
+hipError_t fill_u8(void* p, uint8_t v, size_t n_bytes, hipStream_t s);
+
 // features.hip
 hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int T, float eps,
                            float* feat, int32_t* feat_len, hipStream_t s);
@@ -101,7 +151,8 @@ hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, con
                              float* Gin, hipStream_t s);
 hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
                            const float* hprev, float* hnext, float* cst, float* hfin,
-                           const int32_t* lens, int B, int Tp, int step, int residual, hipStream_t s);
+                           const int32_t* lens, int B, int Tp, int step, int residual, int row0,
+                           int row1, hipStream_t s);
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s);
 
@@ -113,6 +164,7 @@ struct DecodeBufs {
   int32_t* src[2];       // [R]
   float* score[2];       // [R]
   int32_t* newdone;      // [max_len] rows/utterances newly finished at each step
+  int32_t* err;          // [1] CASR_DEV_* guard bits set by kernels (casr_debug_flags)
   // greedy
   uint8_t* fin;          // [R]
   // beam
@@ -136,6 +188,11 @@ struct DecodeArgs {
   float temperature;
   Profiler* prof;        // may be null
 };
+
+// attention.hip: one decode step's additive attention for all R rows (writes ctx into st)
+hipError_t launch_attention_step(const DecodeArgs& a, float* st, float* align, int32_t* newdone,
+                                 int l, int total, hipStream_t s);
+size_t attention_smem_bytes(int k, int Tp);
 
 hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
                       uint8_t* finished, float* accum, float* align, hipStream_t s);

@@ -23,12 +23,6 @@
 
 namespace casr {
 
-__device__ __forceinline__ int done_before(const int32_t* __restrict__ newdone, int l) {
-  int s = 0;
-  for (int i = 0; i < l; ++i) s += newdone[i];
-  return s;
-}
-
 // ------------------------------------------------------------------ split-K row GEMM
 // Block: 16*TM rows x 64 output columns (4 MFMA n-tiles), 4 waves each own every 4th
 // 64-deep k chunk; partial tiles are summed through LDS.
@@ -99,11 +93,27 @@ struct DecLstmA {
   const float* st_old;
   const int32_t* tok;
   const int32_t* src;
-  int R;
+  int32_t* err;
+  int R, V;
   __device__ __forceinline__ const float* ptr(int row, int k) const {
     if (row >= R) return nullptr;
-    if (k < E) return emb + (size_t)tok[row] * E + k;
-    return st_old + (size_t)src[row] * ST + (k - E);
+    if (k < E) {
+      int t = tok[row];
+      if ((unsigned)t >= (unsigned)V) {
+        atomicOr(err, CASR_DEV_BAD_TOKEN);
+        t = 0;
+      }
+      return emb + (size_t)t * E + k;
+    }
+    return st_old + (size_t)safe_src(row) * ST + (k - E);
+  }
+  __device__ __forceinline__ int safe_src(int row) const {
+    const int s = src[row];
+    if ((unsigned)s >= (unsigned)R) {
+      atomicOr(err, CASR_DEV_BAD_SRC);
+      return row;
+    }
+    return s;
   }
 };
 
@@ -112,7 +122,7 @@ struct DecLstmEpi {
   const float* bias;  // packed [4HD]
   const float* st_old;
   float* st_new;
-  const int32_t* src;
+  DecLstmA rows;      // guarded predecessor lookup
   const int32_t* newdone;
   int R, l, total;
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
@@ -126,7 +136,7 @@ struct DecLstmEpi {
       for (int g = 0; g < 4; ++g) gate[g] = red.get(rowl, g * 16 + u) + bias[nb * 64 + g * 16 + u];
       const int U = nb * 16 + u;
       float h2, c2;
-      lstm_cell(gate[0], gate[1], gate[2], gate[3], st_old[(size_t)src[row] * ST + C + HD + U], h2, c2);
+      lstm_cell(gate[0], gate[1], gate[2], gate[3], st_old[(size_t)rows.safe_src(row) * ST + C + HD + U], h2, c2);
       st_new[(size_t)row * ST + C + U] = h2;
       st_new[(size_t)row * ST + C + HD + U] = c2;
     }
@@ -156,153 +166,6 @@ struct ProjEpi {
     }
   }
 };
-
-// ------------------------------------------------------------------ attention
-// One block per utterance b serving its k rows.  Shared: h [k][HD], q [k][A], e/alpha
-// [k][Tp].  keysT is [B][A][Tp] so lanes walking t read coalesced rows.
-template <int KM>
-__global__ __launch_bounds__(256) void attention_kernel(
-    float* __restrict__ st, const float* __restrict__ keysT, const float* __restrict__ enc,
-    const int32_t* __restrict__ lens, const float* __restrict__ Wh, const float* __restrict__ vv,
-    int k, int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l,
-    int total) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  if (done_before(newdone, l) >= total) return;
-  float* hs = sm;                 // [KM][HD]
-  float* qs = hs + KM * HD;       // [KM][A]
-  float* qp = qs + KM * A;        // [KM][A] partials
-  float* es = qp + KM * A;        // [KM][Tp]
-  __shared__ float wred[2][4][KM];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int len = lens[b];
-
-  // 1. h rows -> LDS
-  for (int i = tid; i < k * HD; i += 256) {
-    const int j = i / HD, c = i - j * HD;
-    hs[j * HD + c] = st[(size_t)(b * k + j) * ST + C + c];
-  }
-  __syncthreads();
-
-  // 2. q = h . W_hidden  (thread: column a, half of the 512-long contraction)
-  {
-    const int a = tid & (A - 1), part = tid >> 7;
-    float acc[KM];
-#pragma unroll
-    for (int j = 0; j < KM; ++j) acc[j] = 0.f;
-    for (int i = part * (HD / 2); i < (part + 1) * (HD / 2); ++i) {
-      const float wv = Wh[(size_t)i * A + a];
-#pragma unroll
-      for (int j = 0; j < KM; ++j)
-        if (j < k) acc[j] = fmaf(hs[j * HD + i], wv, acc[j]);
-    }
-    float* dst = part ? qp : qs;
-#pragma unroll
-    for (int j = 0; j < KM; ++j)
-      if (j < k) dst[j * A + a] = acc[j];
-  }
-  __syncthreads();
-  for (int i = tid; i < k * A; i += 256) qs[i] += qp[i];
-  __syncthreads();
-
-  // 3. scores e[j][t] = sum_a v[a] * tanh(keys[t][a] + q[j][a]); masked past len
-  float lmax[KM];
-#pragma unroll
-  for (int j = 0; j < KM; ++j) lmax[j] = -INFINITY;
-  const float* kb = keysT + (size_t)b * A * Tp;
-  for (int t = tid; t < Tp; t += 256) {
-    float e[KM];
-#pragma unroll
-    for (int j = 0; j < KM; ++j) e[j] = 0.f;
-    if (t < len) {
-      for (int a = 0; a < A; ++a) {
-        const float kv = kb[(size_t)a * Tp + t];
-        const float va = vv[a];
-#pragma unroll
-        for (int j = 0; j < KM; ++j)
-          if (j < k) e[j] += tanhf(kv + qs[j * A + a]) * va;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < KM; ++j)
-      if (j < k) {
-        const float ev = (t < len) ? e[j] : -INFINITY;
-        es[j * Tp + t] = ev;
-        lmax[j] = fmaxf(lmax[j], ev);
-      }
-  }
-  // block max per row
-  const int wv_ = tid >> 6, ln = tid & 63;
-#pragma unroll
-  for (int j = 0; j < KM; ++j)
-    if (j < k) {
-      const float m = wave_max(lmax[j]);
-      if (ln == 0) wred[0][wv_][j] = m;
-    }
-  __syncthreads();
-  float rmax[KM], lsum[KM];
-#pragma unroll
-  for (int j = 0; j < KM; ++j) {
-    rmax[j] = (j < k) ? fmaxf(fmaxf(wred[0][0][j], wred[0][1][j]), fmaxf(wred[0][2][j], wred[0][3][j])) : 0.f;
-    lsum[j] = 0.f;
-  }
-  // 4. softmax over t (torch: exp(x - max), then * 1/sum)
-  for (int t = tid; t < Tp; t += 256) {
-#pragma unroll
-    for (int j = 0; j < KM; ++j)
-      if (j < k) {
-        const float p = expf(es[j * Tp + t] - rmax[j]);
-        es[j * Tp + t] = p;
-        lsum[j] += p;
-      }
-  }
-#pragma unroll
-  for (int j = 0; j < KM; ++j)
-    if (j < k) {
-      const float s = wave_sum(lsum[j]);
-      if (ln == 0) wred[1][wv_][j] = s;
-    }
-  __syncthreads();
-  float rinv[KM];
-#pragma unroll
-  for (int j = 0; j < KM; ++j)
-    rinv[j] = (j < k) ? 1.0f / ((wred[1][0][j] + wred[1][1][j]) + (wred[1][2][j] + wred[1][3][j])) : 0.f;
-  for (int t = tid; t < Tp; t += 256) {
-#pragma unroll
-    for (int j = 0; j < KM; ++j)
-      if (j < k) {
-        const float al = es[j * Tp + t] * rinv[j];
-        es[j * Tp + t] = al;
-        if (align) align[(size_t)t * ((size_t)gridDim.x * k) + b * k + j] = al;
-      }
-  }
-  __syncthreads();
-
-  // 5. context ctx[j][c] = sum_t alpha[j][t] * enc[b][t][c]; thread owns 2 columns
-  {
-    const int c0 = 2 * tid;
-    float acc0[KM], acc1[KM];
-#pragma unroll
-    for (int j = 0; j < KM; ++j) acc0[j] = acc1[j] = 0.f;
-    const float* eb = enc + (size_t)b * Tp * C + c0;
-    for (int t = 0; t < len; ++t) {
-      const float2 v2 = *reinterpret_cast<const float2*>(eb + (size_t)t * C);
-#pragma unroll
-      for (int j = 0; j < KM; ++j)
-        if (j < k) {
-          const float al = es[j * Tp + t];
-          acc0[j] += al * v2.x;
-          acc1[j] += al * v2.y;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < KM; ++j)
-      if (j < k) {
-        float* o = st + (size_t)(b * k + j) * ST + c0;
-        o[0] = acc0[j];
-        o[1] = acc1[j];
-      }
-  }
-}
 
 // ------------------------------------------------------------------ init
 // st0[r] = [ctx 0 | h_fin(b) | c_fin(b)], tok = sos, src = r, score = 0 (model.py:531-535,
@@ -345,7 +208,7 @@ __device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
 __global__ __launch_bounds__(256) void greedy_select_kernel(
     const float* __restrict__ logits, int V, int R, int l, int L, int eos, int32_t* __restrict__ tok_next,
     int32_t* __restrict__ src_next, uint8_t* __restrict__ fin, int32_t* __restrict__ out_len, float* __restrict__ accum,
-    int32_t* __restrict__ tokens, int32_t* __restrict__ newdone) {
+    int32_t* __restrict__ tokens, int32_t* __restrict__ newdone, int32_t* __restrict__ err) {
   __shared__ float sv[4];
   __shared__ int si[4];
   __shared__ float ss[4];
@@ -354,11 +217,23 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(
   const float* x = logits + (size_t)r * V;
   float m = -INFINITY;
   int mi = 0x7fffffff;
-  for (int v = tid; v < V; v += 256) {
-    const float xv = x[v];
-    if (xv > m) {
-      m = xv;
-      mi = v;
+  if ((V & 3) == 0) {  // rows are 16 B aligned: 4 logits per load, 4 loads in flight
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+#pragma unroll 4
+    for (int i = tid; i < V / 4; i += 256) {
+      const float4 q = x4[i];
+      if (q.x > m) { m = q.x; mi = 4 * i; }
+      if (q.y > m) { m = q.y; mi = 4 * i + 1; }
+      if (q.z > m) { m = q.z; mi = 4 * i + 2; }
+      if (q.w > m) { m = q.w; mi = 4 * i + 3; }
+    }
+  } else {
+    for (int v = tid; v < V; v += 256) {
+      const float xv = x[v];
+      if (xv > m) {
+        m = xv;
+        mi = v;
+      }
     }
   }
 #pragma unroll
@@ -384,7 +259,16 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(
       mi = si[w];
     }
   float s = 0.f;
-  for (int v = tid; v < V; v += 256) s += expf(x[v] - m);
+  if ((V & 3) == 0) {
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+#pragma unroll 4
+    for (int i = tid; i < V / 4; i += 256) {
+      const float4 q = x4[i];
+      s += expf(q.x - m) + expf(q.y - m) + expf(q.z - m) + expf(q.w - m);
+    }
+  } else {
+    for (int v = tid; v < V; v += 256) s += expf(x[v] - m);
+  }
   s = wave_sum(s);
   if (ln == 0) ss[wv] = s;
   __syncthreads();
@@ -392,7 +276,11 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(
     const float sum = (ss[0] + ss[1]) + (ss[2] + ss[3]);
     const float lse = logf(sum) + m;  // torch.logsumexp: log(sum(exp(x - max))) + max
     const float lp = m - lse;
-    const int tok = mi;
+    int tok = mi;
+    if ((unsigned)tok >= (unsigned)V) {  // no finite maximum (NaN row)
+      atomicOr(err, CASR_DEV_NAN_LOGITS);
+      tok = 0;
+    }
     tokens[(size_t)r * L + l] = tok;
     tok_next[r] = tok;
     src_next[r] = r;  // greedy never reorders
@@ -475,16 +363,21 @@ __device__ __forceinline__ void wave_merge(TopList<K2>& L, int n, float* outv, i
   }
 }
 
+// One block per utterance, one wave per beam row (rows j = w, w + 8): three exact passes
+// over the row (max, sum of exp -> lse; then val = (x/T - lse) + score inserted into a
+// per-lane sorted list), the lane lists merged with wave shuffles to the row's top-2k, then
+// wave 0 merges the k rows' lists from LDS into the utterance's top-2k (torch.topk over
+// the k*V flattened scores, model.py:860-865; ties -> lower flat index).
 template <int K2>
-__global__ __launch_bounds__(256) void beam_select_kernel(
+__global__ __launch_bounds__(512) void beam_select_kernel(
     const float* __restrict__ logits, int V, int B, int k, int l, int L, int eos, float temperature,
     const float* __restrict__ score_cur, float* __restrict__ score_next,
     int32_t* __restrict__ tok_next, int32_t* __restrict__ src_next, uint8_t* __restrict__ topfin,
     int32_t* __restrict__ bp, int32_t* __restrict__ tk, float* __restrict__ rec_score,
-    int32_t* __restrict__ rec_src, uint8_t* __restrict__ rec_valid, int32_t* __restrict__ newdone) {
-  __shared__ float lse_s[KMAX_BEAM];
-  __shared__ float wv_s[4][K2];
-  __shared__ int wi_s[4][K2];
+    int32_t* __restrict__ rec_src, uint8_t* __restrict__ rec_valid, int32_t* __restrict__ newdone,
+    int32_t* __restrict__ err) {
+  __shared__ float rv_s[KMAX_BEAM][K2];
+  __shared__ int ri_s[KMAX_BEAM][K2];
   __shared__ float cv[K2];
   __shared__ int ci[K2];
   if (done_before(newdone, l) >= B) return;
@@ -492,40 +385,68 @@ __global__ __launch_bounds__(256) void beam_select_kernel(
   const int R = B * k;
   const int nrows = (l == 0) ? 1 : k;  // model.py:862-863: step 0 ranks beam 0 only
   const int n2k = 2 * k;
+  const bool vec = (V & 3) == 0;
 
-  for (int j = wv; j < nrows; j += 4) {
+  for (int j = wv; j < nrows; j += 8) {
     const float* x = logits + (size_t)(b * k + j) * V;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
     float m = -INFINITY;
-    for (int v = ln; v < V; v += 64) m = fmaxf(m, x[v] / temperature);
+    if (vec) {
+#pragma unroll 4
+      for (int i = ln; i < V / 4; i += 64) {
+        const float4 q = x4[i];
+        m = fmaxf(m, fmaxf(fmaxf(q.x / temperature, q.y / temperature),
+                           fmaxf(q.z / temperature, q.w / temperature)));
+      }
+    } else {
+      for (int v = ln; v < V; v += 64) m = fmaxf(m, x[v] / temperature);
+    }
     m = wave_max(m);
     float s = 0.f;
-    for (int v = ln; v < V; v += 64) s += expf(x[v] / temperature - m);
-    s = wave_sum(s);
-    if (ln == 0) lse_s[j] = logf(s) + m;
-  }
-  __syncthreads();
-
-  TopList<K2> tl;
-  tl.init();
-  for (int j = 0; j < nrows; ++j) {
-    const float* x = logits + (size_t)(b * k + j) * V;
-    const float lse = lse_s[j], sc = score_cur[b * k + j];
-    for (int v = tid; v < V; v += 256) {
-      const float val = (x[v] / temperature - lse) + sc;  // model.py:834-836
-      tl.insert(val, j * V + v);
+    if (vec) {
+#pragma unroll 4
+      for (int i = ln; i < V / 4; i += 64) {
+        const float4 q = x4[i];
+        s += expf(q.x / temperature - m) + expf(q.y / temperature - m) + expf(q.z / temperature - m) +
+             expf(q.w / temperature - m);
+      }
+    } else {
+      for (int v = ln; v < V; v += 64) s += expf(x[v] / temperature - m);
     }
+    s = wave_sum(s);
+    const float lse = logf(s) + m;
+    const float sc = score_cur[b * k + j];
+    TopList<K2> tl;
+    tl.init();
+    if (vec) {
+#pragma unroll 2
+      for (int i = ln; i < V / 4; i += 64) {
+        const float4 q = x4[i];
+        tl.insert((q.x / temperature - lse) + sc, j * V + 4 * i);  // model.py:834-836
+        tl.insert((q.y / temperature - lse) + sc, j * V + 4 * i + 1);
+        tl.insert((q.z / temperature - lse) + sc, j * V + 4 * i + 2);
+        tl.insert((q.w / temperature - lse) + sc, j * V + 4 * i + 3);
+      }
+    } else {
+      for (int v = ln; v < V; v += 64) tl.insert((x[v] / temperature - lse) + sc, j * V + v);
+    }
+    wave_merge<K2>(tl, n2k, rv_s[j], ri_s[j]);
   }
-  wave_merge<K2>(tl, n2k, wv_s[wv], wi_s[wv]);
   __syncthreads();
   if (wv == 0) {
     TopList<K2> t2;
     t2.init();
-    for (int p = ln; p < 4 * n2k; p += 64) t2.insert(wv_s[p / n2k][p % n2k], wi_s[p / n2k][p % n2k]);
+    for (int p = ln; p < nrows * n2k; p += 64) t2.insert(rv_s[p / n2k][p % n2k], ri_s[p / n2k][p % n2k]);
     wave_merge<K2>(t2, n2k, cv, ci);
   }
   __syncthreads();
 
   if (tid == 0) {
+    for (int c = 0; c < n2k; ++c)
+      if ((unsigned)ci[c] >= (unsigned)(nrows * V)) {  // NaN rows leave empty list slots
+        atomicOr(err, CASR_DEV_BAD_CAND);
+        ci[c] = 0;
+      }
     // finished hypotheses among the first k candidates (model.py:874-889)
     for (int c = 0; c < k; ++c) {
       const int beam = ci[c] / V, tok = ci[c] - beam * V;
@@ -580,7 +501,7 @@ __global__ void beam_finalize_kernel(int B, int k, int L, float lm_weight, float
                                      const uint8_t* __restrict__ rec_valid,
                                      const int32_t* __restrict__ newdone, int32_t* __restrict__ best_tokens,
                                      int32_t* __restrict__ best_len, float* __restrict__ best_score,
-                                     int32_t* __restrict__ steps_out) {
+                                     int32_t* __restrict__ steps_out, int32_t* __restrict__ err) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   const int steps = executed_steps(newdone, L, B);
   if (b == 0) steps_out[0] = steps;
@@ -623,6 +544,10 @@ __global__ void beam_finalize_kernel(int B, int k, int L, float lm_weight, float
     from = ll;
   }
   for (int s = from; s >= 0; --s) {
+    if ((unsigned)slot >= (unsigned)k) {
+      atomicOr(err, CASR_DEV_BAD_BACKPTR);
+      slot = 0;
+    }
     const size_t ix = (size_t)s * R + b * k + slot;
     out[s] = tk[ix];
     slot = bp[ix];
@@ -638,7 +563,8 @@ __global__ void beam_records_kernel(int B, int k, int L, const int32_t* __restri
                                     const int32_t* __restrict__ rec_src,
                                     const uint8_t* __restrict__ rec_valid,
                                     const int32_t* __restrict__ newdone, int32_t* __restrict__ out_tok,
-                                    float* __restrict__ out_score, uint8_t* __restrict__ out_valid) {
+                                    float* __restrict__ out_score, uint8_t* __restrict__ out_valid,
+                                    int32_t* __restrict__ err) {
   const int b = blockIdx.x, l = blockIdx.y, c = threadIdx.x;
   if (c >= k) return;
   const int steps = executed_steps(newdone, L, B);
@@ -655,6 +581,10 @@ __global__ void beam_records_kernel(int B, int k, int L, const int32_t* __restri
   int slot = rec_src[ri];
   const int R = B * k;
   for (int s = l - 1; s >= 0; --s) {
+    if ((unsigned)slot >= (unsigned)k) {
+      atomicOr(err, CASR_DEV_BAD_BACKPTR);
+      slot = 0;
+    }
     const size_t ix = (size_t)s * R + b * k + slot;
     o[s] = tk[ix];
     slot = bp[ix];
@@ -663,28 +593,6 @@ __global__ void beam_records_kernel(int B, int k, int L, const int32_t* __restri
 }
 
 // ------------------------------------------------------------------ host drivers
-template <int KM>
-static hipError_t launch_attention(const DecodeArgs& a, float* st, float* align, int32_t* newdone,
-                                   int l, int total, hipStream_t s) {
-  const size_t shm = (size_t)(KM * HD + 2 * KM * A + KM * a.Tp) * sizeof(float);
-  hipLaunchKernelGGL(attention_kernel<KM>, dim3(a.B), dim3(256), shm, s, st, a.keysT, a.enc, a.lens,
-                     a.W + a.L.w_hidden, a.W + a.L.v, a.k, a.Tp, align, newdone, l, total);
-  return hipGetLastError();
-}
-
-static hipError_t attention_dispatch(const DecodeArgs& a, float* st, float* align, int32_t* newdone,
-                                     int l, int total, hipStream_t s) {
-  if (a.k <= 1) return launch_attention<1>(a, st, align, newdone, l, total, s);
-  if (a.k <= 4) return launch_attention<4>(a, st, align, newdone, l, total, s);
-  if (a.k <= 8) return launch_attention<8>(a, st, align, newdone, l, total, s);
-  return launch_attention<16>(a, st, align, newdone, l, total, s);
-}
-
-size_t attention_smem_bytes(int k, int Tp) {
-  const int km = k <= 1 ? 1 : k <= 4 ? 4 : k <= 8 ? 8 : 16;
-  return (size_t)(km * HD + 2 * km * A + km * Tp) * sizeof(float);
-}
-
 static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
                               hipStream_t s) {
   const int R = a.B * a.k;
@@ -693,8 +601,8 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   {
     ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
     constexpr int TM = 1;
-    DecLstmA asrc{a.W + a.L.emb, st_old, d.tok[l & 1], d.src[l & 1], R};
-    DecLstmEpi<TM> epi{a.W + a.L.dec_b, st_old, st_new, d.src[l & 1], d.newdone, R, l, total};
+    DecLstmA asrc{a.W + a.L.emb, st_old, d.tok[l & 1], d.src[l & 1], d.err, R, a.V};
+    DecLstmEpi<TM> epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, R, l, total};
     dim3 grid(HD / 16, (R + 16 * TM - 1) / (16 * TM));
     hipLaunchKernelGGL((rowgemm_kernel<TM, DecLstmA, DecLstmEpi<TM>>), grid, dim3(256), 0, s,
                        KDEC / 64, a.W + a.L.dec_w, asrc, epi);
@@ -702,7 +610,7 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   hipError_t e;
   {
     ProfScope ps(a.prof, CASR_K_ATTENTION, s);
-    e = attention_dispatch(a, st_new, align, d.newdone, l, total, s);
+    e = launch_attention_step(a, st_new, align, d.newdone, l, total, s);
   }
   if (e != hipSuccess) return e;
   {
@@ -720,11 +628,13 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
 hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
                       uint8_t* finished, float* accum, float* align, hipStream_t s) {
   const int R = a.B;
-  hipError_t e0 = hipMemsetAsync(d.newdone, 0, sizeof(int32_t) * a.max_len, s);
-  if (e0 == hipSuccess) e0 = hipMemsetAsync(finished, 0, R, s);
-  if (e0 == hipSuccess) e0 = hipMemsetAsync(out_len, 0, sizeof(int32_t) * R, s);
-  if (e0 == hipSuccess) e0 = hipMemsetAsync(accum, 0, sizeof(float) * R, s);
-  if (e0 == hipSuccess) e0 = hipMemsetAsync(tokens, 0xff, sizeof(int32_t) * R * a.max_len, s);
+  // fill kernels, not hipMemsetAsync: this sequence is captured into a replayed graph
+  hipError_t e0 = fill_u32(d.newdone, 0, a.max_len, s);
+  if (e0 == hipSuccess) e0 = fill_u32(d.err, 0, 1, s);
+  if (e0 == hipSuccess) e0 = fill_u8(finished, 0, R, s);
+  if (e0 == hipSuccess) e0 = fill_u32(out_len, 0, R, s);
+  if (e0 == hipSuccess) e0 = fill_u32(accum, 0, R, s);
+  if (e0 == hipSuccess) e0 = fill_u32(tokens, 0xffffffffu, (size_t)R * a.max_len, s);
   if (e0 != hipSuccess) return e0;
   hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, 1,
                      a.sos, d.tok[0], d.src[0], d.score[0]);
@@ -734,25 +644,26 @@ hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32
     ProfScope ps(a.prof, CASR_K_SELECT, s);
     hipLaunchKernelGGL(greedy_select_kernel, dim3(R), dim3(256), 0, s, d.logits, a.V, R, l,
                        a.max_len, a.eos, d.tok[(l + 1) & 1], d.src[(l + 1) & 1], finished, out_len,
-                       accum, tokens, d.newdone);
+                       accum, tokens, d.newdone, d.err);
   }
   return hipGetLastError();
 }
 
 template <int K2>
 static void launch_beam_select(const DecodeArgs& a, DecodeBufs& d, int l, hipStream_t s) {
-  hipLaunchKernelGGL(beam_select_kernel<K2>, dim3(a.B), dim3(256), 0, s, d.logits, a.V, a.B, a.k, l,
+  hipLaunchKernelGGL(beam_select_kernel<K2>, dim3(a.B), dim3(512), 0, s, d.logits, a.V, a.B, a.k, l,
                      a.max_len, a.eos, a.temperature, d.score[l & 1], d.score[(l + 1) & 1],
                      d.tok[(l + 1) & 1], d.src[(l + 1) & 1], d.topfin, d.bp, d.tk, d.rec_score,
-                     d.rec_src, d.rec_valid, d.newdone);
+                     d.rec_src, d.rec_valid, d.newdone, d.err);
 }
 
 hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float length_weight,
                     int32_t* best_tokens, int32_t* best_len, float* best_score, int32_t* steps,
                     hipStream_t s) {
   const int R = a.B * a.k;
-  hipError_t e0 = hipMemsetAsync(d.newdone, 0, sizeof(int32_t) * a.max_len, s);
-  if (e0 == hipSuccess) e0 = hipMemsetAsync(d.topfin, 0, a.B, s);
+  hipError_t e0 = fill_u32(d.newdone, 0, a.max_len, s);
+  if (e0 == hipSuccess) e0 = fill_u32(d.err, 0, 1, s);
+  if (e0 == hipSuccess) e0 = fill_u8(d.topfin, 0, a.B, s);
   if (e0 != hipSuccess) return e0;
   hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, a.k,
                      a.sos, d.tok[0], d.src[0], d.score[0]);
@@ -767,7 +678,7 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
   }
   hipLaunchKernelGGL(beam_finalize_kernel, dim3((a.B + 63) / 64), dim3(64), 0, s, a.B, a.k, a.max_len,
                      lm_weight, length_weight, d.score[0], d.score[1], d.bp, d.tk, d.rec_score, d.rec_src,
-                     d.rec_valid, d.newdone, best_tokens, best_len, best_score, steps);
+                     d.rec_valid, d.newdone, best_tokens, best_len, best_score, steps, d.err);
   return hipGetLastError();
 }
 
@@ -775,7 +686,7 @@ hipError_t run_beam_records(const DecodeArgs& a, DecodeBufs& d, int32_t* rec_tok
                             float* rec_score, uint8_t* rec_valid, hipStream_t s) {
   hipLaunchKernelGGL(beam_records_kernel, dim3(a.B, a.max_len), dim3(64), 0, s, a.B, a.k, a.max_len,
                      d.bp, d.tk, d.rec_score, d.rec_src, d.rec_valid, d.newdone, rec_tokens,
-                     rec_score, rec_valid);
+                     rec_score, rec_valid, d.err);
   return hipGetLastError();
 }
 

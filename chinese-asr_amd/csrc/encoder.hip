@@ -34,13 +34,13 @@ struct StoreBiasEpi {  // C[row][col] = acc + bias[col]
   }
 };
 
-struct KeysEpi {  // keysT[b][a][t] = acc + b_attn[a], row = b*Tp + t
+struct KeysEpi {  // keysT[b][a][t] = acc + b_attn[a], row = b*Tp + t, row stride Tq
   float* keysT;
   const float* bias;
-  int Tp;
+  int Tp, Tq;
   __device__ __forceinline__ void operator()(int row, int col, float v) const {
     const int b = row / Tp, t = row - b * Tp;
-    keysT[((size_t)b * A + col) * Tp + t] = v + bias[col];
+    keysT[((size_t)b * A + col) * Tq + t] = v + bias[col];
   }
 };
 
@@ -144,7 +144,7 @@ hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, con
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s) {
   const int M = B * Tp;
-  KeysEpi epi{keysT, b_attn, Tp};
+  KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3};
   dim3 grid(A / GB_N, (M + GB_M - 1) / GB_M);
   hipLaunchKernelGGL(gemm_nt_kernel<KeysEpi>, grid, dim3(256), 0, s, enc, C, wencT, C, M, A, C,
                      epi);
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void rec_step_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, const float* __restrict__ hprev, float* __restrict__ hnext,
     float* __restrict__ cst, float* __restrict__ hfin, const int32_t* __restrict__ lens, int B,
-    int Tp, int step, int residual) {
+    int Tp, int step, int residual, int row0, int row1) {
   constexpr int NKC = H / 64;  // k chunks of 64
   __shared__ f32x4 red[4][4][64];
   const int jb = blockIdx.x, rb = blockIdx.y, d = blockIdx.z;
@@ -165,17 +165,37 @@ __global__ __launch_bounds__(256) void rec_step_kernel(
   const int r = lane & 15, g = lane >> 4;
   const float* Wd = Whh_f + (size_t)d * (H / 16) * 4 * NKC * FRAG;
 
+  // epilogue cell of this thread: (row rl, unit u).  Its operands (4 gate pre-activations
+  // from Gin, c, the residual input) do not depend on this step's GEMM, so they are loaded
+  // first and their latency hides behind the W_hh / h loads and the MFMAs.
+  const int rl = threadIdx.x >> 4, u = threadIdx.x & 15;
+  const int b = row0 + rb * 16 + rl;  // rows [row0, row1) of the batch
+  const int len = b < row1 ? min(lens[b], Tp) : 0;
+  const bool act = step < len;
+  const int t = (d == 0) ? step : (len - 1 - step);
+  const int U = jb * 16 + u;
+  const size_t si = ((size_t)d * B + b) * H + U;
+  const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
+  float gin_v[4] = {0.f, 0.f, 0.f, 0.f}, c_old = 0.f, x_res = 0.f;
+  if (act) {
+    const float* gin = Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + jb * 64;
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) gin_v[tn] = gin[tn * 16 + u];
+    c_old = cst[si];
+    if (residual) x_res = xin[oi];
+  }
+
   f32x4 acc[4];
 #pragma unroll
   for (int tn = 0; tn < 4; ++tn) acc[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int row = rb * 16 + r;
+  const int row = row0 + rb * 16 + r;
   for (int kc = w; kc < NKC; kc += 4) {
     float4 a[4], bw[4][4];
     const float* ap = hprev + ((size_t)d * B + row) * H + kc * 64 + g * 16;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      a[q] = row < B ? *reinterpret_cast<const float4*>(ap + q * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      a[q] = row < row1 ? *reinterpret_cast<const float4*>(ap + q * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) {
       const float* wb = Wd + ((size_t)(jb * 4 + tn) * NKC + kc) * FRAG + lane * 4;
@@ -196,41 +216,31 @@ __global__ __launch_bounds__(256) void rec_step_kernel(
   for (int tn = 0; tn < 4; ++tn) red[w][tn][lane] = acc[tn];
   __syncthreads();
 
-  // epilogue: thread -> (row rl, unit u) cell
-  const int rl = threadIdx.x >> 4, u = threadIdx.x & 15;
-  const int b = rb * 16 + rl;
-  if (b >= B) return;
-  const int len = lens[b];
-  if (step >= len) return;
-  const int t = (d == 0) ? step : (len - 1 - step);
+  if (!act) return;
   const int src_lane = u + 16 * (rl >> 2), reg = rl & 3;
   float gate[4];
-  const float* gin = Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + jb * 64;
 #pragma unroll
   for (int tn = 0; tn < 4; ++tn) {
     float sum = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 4; ++ww) sum += red[ww][tn][src_lane][reg];
-    gate[tn] = sum + gin[tn * 16 + u];
+    gate[tn] = sum + gin_v[tn];
   }
-  const int U = jb * 16 + u;
-  const size_t si = ((size_t)d * B + b) * H + U;
   float h2, c2;
-  lstm_cell(gate[0], gate[1], gate[2], gate[3], cst[si], h2, c2);
+  lstm_cell(gate[0], gate[1], gate[2], gate[3], c_old, h2, c2);
   cst[si] = c2;
   hnext[si] = h2;
   if (step == len - 1) hfin[si] = h2;
-  const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
-  out[oi] = residual ? (h2 + xin[oi]) : h2;
+  out[oi] = residual ? (h2 + x_res) : h2;
 }
 
 hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
                            const float* hprev, float* hnext, float* cst, float* hfin,
-                           const int32_t* lens, int B, int Tp, int step, int residual,
+                           const int32_t* lens, int B, int Tp, int step, int residual, int row0, int row1,
                            hipStream_t s) {
-  dim3 grid(H / 16, (B + 15) / 16, 2);
+  dim3 grid(H / 16, (row1 - row0 + 15) / 16, 2);
   hipLaunchKernelGGL(rec_step_kernel, grid, dim3(256), 0, s, Whh_f, Gin, xin, out, hprev, hnext,
-                     cst, hfin, lens, B, Tp, step, residual);
+                     cst, hfin, lens, B, Tp, step, residual, row0, row1);
   return hipGetLastError();
 }
 

@@ -141,6 +141,17 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
 int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uint8_t* rec_valid,
                       void* stream);
 
+/* Guard bits raised by the decode kernels since the last casr_greedy / casr_beam (0 = clean):
+ * a data-dependent index out of range (1 token, 2 predecessor row, 4 NaN logit row, 8 beam
+ * candidate, 16 back-pointer) is clamped and reported here instead of faulting the device.
+ * Synchronises `stream`. */
+int casr_device_flags(casr_handle* h, int32_t* flags_host, void* stream);
+
+/* The launch-bound loops (each layer's Tp recurrence steps, the whole decode loop) are
+ * captured once per shape into hipGraphs on a private stream and replayed on `stream`
+ * (default on).  0 = launch every kernel eagerly (same results, bit for bit). */
+int casr_set_graphs(casr_handle* h, int enable);
+
 /* Launch timing per kernel class with HIP event pairs recorded on the launch stream around
  * every launch of the enabled classes (bench.py's roofline figures).  Enabling resets
  * the counters; reading synchronises on the recorded events. */

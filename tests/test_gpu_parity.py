@@ -85,6 +85,7 @@ def test_greedy_matches_reference(eng, name):
     feat, flen = golden_features(eng)
     eng.encode(feat, flen)
     out = eng.greedy(alignment=True)
+    assert eng.device_flags() == 0
     tokens = out["tokens"].cpu().numpy()
     out_len = out["out_len"].cpu().numpy()
     fin = out["finished"].cpu().numpy().astype(bool)
@@ -107,6 +108,7 @@ def test_beam_matches_reference(eng, name, k):
     feat, flen = golden_features(eng)
     eng.encode(feat, flen)
     r = eng.beam(k)
+    assert eng.device_flags() == 0
     toks = r["tokens"].cpu().numpy()
     blen = r["length"].cpu().numpy()
     gold = META[name][f"beam{k}"]
@@ -156,6 +158,27 @@ def test_model_dropin_api_matches_reference():
     assert [[ord(ch) - 0xE000 for ch in t] for t in r.pred_text] == META["peaked"]["beam4_lm"]["tokens"]
 
 
+def test_graph_replay_equals_eager(eng):
+    """hipGraph replay (default) and eager launches give bitwise-identical results."""
+    bind(eng, "peaked")
+    feat, flen = golden_features(eng)
+    outs = []
+    for graphs in (False, True, True):  # second graph run replays the cached graph
+        eng.set_graphs(graphs)
+        eng.encode(feat, flen)
+        enc = eng.encoder_results()[0].cpu()
+        g = eng.greedy(alignment=True)
+        bm = eng.beam(4, 1.5, 1.5)
+        assert eng.device_flags() == 0
+        outs.append((enc, g["tokens"].cpu(), g["accum"].cpu(), g["alignment"].cpu(), bm["tokens"].cpu(),
+                     bm["score"].cpu(), bm["steps"].cpu()))
+    eng.set_graphs(True)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    for a, b in zip(outs[1], outs[2]):
+        assert torch.equal(a, b)
+
+
 def _bench_batch(eng, B, T=800):
     x = np.stack([fbank_for(b, T) for b in range(B)])
     fb = torch.from_numpy(x).to(eng.device)
@@ -170,6 +193,7 @@ def test_full_length_greedy_matches_oracle(eng):
     feat, flen = _bench_batch(eng, B)
     eng.encode(feat, flen)
     out = eng.greedy()
+    assert eng.device_flags() == 0
     toks = out["tokens"].cpu().numpy()
     feats = [O.features_from_fbank(fbank_for(b, 800)) for b in range(B)]
     r = O.greedy_decode(feats, [266] * B, enc_sd, dec_sd)
