@@ -55,6 +55,18 @@ def kernel_work(cls, B, Tp, R, V, T):
     return 0.0, "hbm"
 
 
+# what one profiled "launch" of a class is (the unit achieved/avg_launch_us refer to; the rocprof
+# kernel-trace average of the same kernel must agree: profiles/r01/)
+LAUNCH_UNIT = {
+    "rec_step": "rec_layer_kernel: one encoder layer, all Tp steps, both directions, B rows "
+                "(per-step launches rec_step_kernel when the persistent grid does not fit)",
+    "input_proj": "gemm_nt_kernel<StoreBiasEpi>: one layer's input projection, B*Tp rows",
+    "proj": "rowgemm_kernel<2,ProjA>: one decode step's vocabulary projection",
+    "dec_lstm": "rowgemm_kernel<1,DecLstmA>: one decode step's LSTMCell",
+    "attention": "attention_kernel: one decode step",
+}
+
+
 def cpu_baseline(n_utt, T):
     """The CPU oracle (numpy restatement of the reference path, oracle/casr_oracle.py) timed
     on this host on a bounded sample of the same workload."""
@@ -221,7 +233,8 @@ def main():
             "beam": beam,
             "roofline": {"kernel": dominant, "bound": bound, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": achieved / peak, "traffic": traffic,
-                         "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s},
+                         "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s,
+                         "launch": LAUNCH_UNIT.get(dominant, "one kernel launch")},
             "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},
             "weights_bcast_s": weight_s,
             "device_flags": flags,

@@ -148,6 +148,14 @@ class Engine:
         """hipGraph replay of the launch-bound loops (default on); off = eager launches."""
         _lib.check(self.lib.casr_set_graphs(self.handle, int(bool(enable))), self.handle)
 
+    def set_persistent(self, enable):
+        """Persistent per-layer recurrence (default on where its grid fits); off = per-step."""
+        _lib.check(self.lib.casr_set_persistent(self.handle, int(bool(enable))), self.handle)
+
+    def recurrence_mode(self, B):
+        """1 if casr_encode would run the persistent recurrence for batch B, else 0."""
+        return int(self.lib.casr_recurrence_mode(self.handle, int(B)))
+
     # ------------------------------------------------------------------ launch timing
     def profile(self, classes):
         """Enable HIP-event timing for the named kernel classes (lib.KERNEL_CLASSES)."""

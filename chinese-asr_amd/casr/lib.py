@@ -20,7 +20,7 @@ EXPORTS = [
     "casr_bind_weights", "casr_destroy", "casr_last_error", "casr_features",
     "casr_gather_utterances", "casr_encode", "casr_encoder_results", "casr_greedy", "casr_beam",
     "casr_beam_records", "casr_profile_enable", "casr_profile_read", "casr_set_graphs",
-    "casr_device_flags",
+    "casr_device_flags", "casr_set_persistent", "casr_recurrence_mode",
 ]
 
 # kernel classes of casr_profile_enable / casr_profile_read (include/casr.h)
@@ -87,6 +87,8 @@ def load(path=None):
         "casr_profile_enable": (i32, [vp, ctypes.c_uint32]),
         "casr_set_graphs": (i32, [vp, i32]),
         "casr_device_flags": (i32, [vp, ctypes.POINTER(ctypes.c_int32), vp]),
+        "casr_set_persistent": (i32, [vp, i32]),
+        "casr_recurrence_mode": (i32, [vp, i32]),
         "casr_profile_read": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():

@@ -4,6 +4,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -102,6 +103,10 @@ struct casr_handle {
   std::string err;
   // encoder workspace
   DevBuf gin, out0, out1, hbuf, cst, hfin, keysT, lens;
+  DevBuf hx;       // persistent recurrence: tagged h words [3][2][Bp][H]
+  DevBuf eflag;    // encoder device guard bits (CASR_DEV_REC_TIMEOUT)
+  bool use_persistent = true;
+  int rec_capacity = 0;  // workgroups of rec_layer_kernel resident at once (CUs x blocks/CU)
   int B = 0, Tp = 0;
   bool encoded = false;
   float* enc_out = nullptr;  // out0 or out1
@@ -294,6 +299,10 @@ int casr_create(const casr_config* cfg, int device, casr_handle** out) {
   h->cfg = *cfg;
   h->L = make_layout(*cfg);
   h->device = device;
+  // the persistent recurrence needs every workgroup of its grid resident at once
+  int per_cu = 0;
+  if (hipSetDevice(device) == hipSuccess && rec_layer_occupancy(&per_cu) == hipSuccess)
+    h->rec_capacity = per_cu * prop.multiProcessorCount;
   *out = h;
   return CASR_OK;
 }
@@ -314,7 +323,7 @@ void casr_destroy(casr_handle* h) {
     if (h->ev_out[i]) (void)hipEventDestroy(h->ev_out[i]);
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
-  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens,
+  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->hx, &h->eflag,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout})
     b->release();
   delete h;
@@ -324,6 +333,17 @@ int casr_set_graphs(casr_handle* h, int enable) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   h->use_graphs = enable != 0;
   return CASR_OK;
+}
+
+int casr_set_persistent(casr_handle* h, int enable) {
+  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
+  h->use_persistent = enable != 0;
+  return CASR_OK;
+}
+
+int casr_recurrence_mode(const casr_handle* h, int B) {
+  if (!h || B <= 0) return -1;
+  return (h->use_persistent && rec_layer_grid_blocks(B) <= h->rec_capacity) ? 1 : 0;
 }
 
 const char* casr_last_error(const casr_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
@@ -367,6 +387,10 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   HIP_OK(h, hipMemsetAsync(h->out0.p, 0, rows * C * sizeof(float), s));
   HIP_OK(h, hipMemsetAsync(h->out1.p, 0, rows * C * sizeof(float), s));
   HIP_OK(h, hipMemsetAsync(h->hfin.p, 0, (size_t)2 * B * H * sizeof(float), s));
+  HIP_OK(h, h->eflag.ensure(16));
+  HIP_OK(h, hipMemsetAsync(h->eflag.p, 0, 16, s));
+  const bool persistent = casr_recurrence_mode(h, B) == 1;
+  if (persistent) HIP_OK(h, h->hx.ensure(rec_layer_granule_bytes(B)));
   const int32_t* dl = h->lens.as<int32_t>();
   float* outs[2] = {h->out0.as<float>(), h->out1.as<float>()};
   const float* x = feat;
@@ -383,6 +407,39 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
     // layer 0 has no residual input: pass an internal pointer so a graph never bakes in the
     // caller's feature buffer
     const float* xin = residual ? x : out;
+    if (persistent) {
+      // one launch runs all Tp steps; h and c start at zero inside (util.py:1236-1247)
+      HIP_OK(h, reset_rec_layer(reinterpret_cast<uint32_t*>(h->hx.p), B, s));
+      // diagnostics only: CASR_REC_TRACE=<file> dumps per-wave phase timestamps of layer 0
+      const char* trace_path = l == 0 ? std::getenv("CASR_REC_TRACE") : nullptr;
+      DevBuf tbuf;
+      const size_t tbytes = (size_t)rec_layer_grid_blocks(B) * 8 * Tp * 5 * sizeof(uint32_t);
+      if (trace_path) {
+        HIP_OK(h, tbuf.ensure(tbytes));
+        HIP_OK(h, hipMemsetAsync(tbuf.p, 0, tbytes, s));
+      }
+      {
+        ProfScope ps(&h->prof, CASR_K_REC_STEP, s);
+        HIP_OK(h, launch_rec_layer(h->W + h->L.enc_whh[l], h->gin.as<float>(), xin, out,
+                                   reinterpret_cast<uint32_t*>(h->hx.p), h->hfin.as<float>(),
+                                   h->cst.as<float>(), dl, B, Tp, residual, h->eflag.as<int32_t>(),
+                                   tbuf.as<uint32_t>(), s));
+      }
+      if (trace_path) {
+        std::vector<uint32_t> hostv(tbytes / 4);
+        HIP_OK(h, hipMemcpyAsync(hostv.data(), tbuf.p, tbytes, hipMemcpyDeviceToHost, s));
+        HIP_OK(h, hipStreamSynchronize(s));
+        tbuf.release();
+        if (FILE* f = std::fopen(trace_path, "wb")) {
+          const int32_t hdr[4] = {rec_layer_grid_blocks(B), 8, Tp, 5};
+          std::fwrite(hdr, sizeof hdr, 1, f);
+          std::fwrite(hostv.data(), 4, hostv.size(), f);
+          std::fclose(f);
+        }
+      }
+      x = out;
+      continue;
+    }
     // h (both ping-pong buffers) and c start at zero (RNN_RES state None, util.py:1236-1247)
     HIP_OK(h, fill_u32(hb, 0, (size_t)2 * 2 * B * H, s));
     HIP_OK(h, fill_u32(h->cst.p, 0, (size_t)2 * B * H, s));
@@ -608,11 +665,13 @@ int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uin
 int casr_device_flags(casr_handle* h, int32_t* flags, void* stream) {
   if (!h || !flags) return fail(h, CASR_ERR_ARG, "casr_device_flags: bad arguments");
   *flags = 0;
-  if (!h->d.err) return CASR_OK;
   HIP_OK(h, hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
-  HIP_OK(h, hipMemcpyAsync(flags, h->d.err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  int32_t dec = 0, enc = 0;
+  if (h->d.err) HIP_OK(h, hipMemcpyAsync(&dec, h->d.err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (h->eflag.p) HIP_OK(h, hipMemcpyAsync(&enc, h->eflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_OK(h, hipStreamSynchronize(s));
+  *flags = dec | enc;
   return CASR_OK;
 }
 

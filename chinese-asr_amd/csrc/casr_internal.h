@@ -31,6 +31,7 @@ constexpr int CASR_DEV_BAD_SRC = 2;      // predecessor row not in [0, R)
 constexpr int CASR_DEV_NAN_LOGITS = 4;   // no finite maximum in a logit row (greedy)
 constexpr int CASR_DEV_BAD_CAND = 8;     // beam candidate index not in [0, k*V)
 constexpr int CASR_DEV_BAD_BACKPTR = 16; // back-pointer walk left [0, k)
+constexpr int CASR_DEV_REC_TIMEOUT = 32; // persistent recurrence: a bounded hand-off wait expired
 
 // MFMA-fragment-major weight block: a 16-row x 64-k tile stored as [q=0..3][lane][4] so
 // lane l reads row (l&15), k = 16*(l>>4) + 4q + e with one coalesced 16 B load per q.
@@ -153,6 +154,14 @@ hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xi
                            const float* hprev, float* hnext, float* cst, float* hfin,
                            const int32_t* lens, int B, int Tp, int step, int residual, int row0,
                            int row1, hipStream_t s);
+// recurrence.hip: persistent per-layer recurrence (all Tp steps in one launch)
+size_t rec_layer_granule_bytes(int B);
+int rec_layer_grid_blocks(int B);
+hipError_t rec_layer_occupancy(int* blocks_per_cu);
+hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s);  // before EVERY launch_rec_layer
+hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
+                            uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
+                            int residual, int32_t* err, uint32_t* trace, hipStream_t s);
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s);
 

@@ -1,0 +1,245 @@
+// Persistent bidirectional-LSTM recurrence: one launch per encoder layer runs all Tp steps.
+//
+// Reference: RNN_RES.forward util.py:1223-1324 (one nn.LSTM(bidirectional) per layer over a
+// packed batch, encoder.py:36-81), i.e. per direction d and step the gate pre-activations
+//   g[b] = Gin[b, t] + W_hh[d] . h_{t-1}[b]        (Gin = x W_ih^T + b_ih + b_hh, encoder.hip)
+// followed by the (i, f, g, o) cell.  The per-step launch (encoder.hip rec_step_kernel) pays a
+// kernel boundary, a W_hh re-read and a c round trip every step; here each workgroup keeps its
+// W_hh slice and its cells' c in registers for the whole layer and hands h to the other
+// workgroups of its row group through tagged granules (MI355X_MICROARCH.md price list,
+// handoff-1to1 / cdna_hip_programming.md Guideline 16 R2: the data is its own flag):
+//
+//   granule = ONE 4-byte word: the h bits with bit 30 replaced by the step-parity tag.  h =
+//   o * tanh(c) has |h| <= 1, so bit 30 (the exponent MSB, set only for |x| >= 2) is always
+//   0 in a finite h and is free to carry the tag; a non-finite h is sent as 0x3FFFFFFF (a
+//   value in [1, 2) no LSTM output takes) and decoded back to NaN.  Producers store each word
+//   write-through (sc1); a consumer wave re-reads (sc1 loads, L1 bypassed) its 16 rows x 64
+//   units until every tag matches: no counter, no fence, no barrier, 4 B per value.
+//
+// Geometry (gfx950, 256 CUs): workgroup (ub, rg, d) = 16 hidden units (64 gate rows, all four
+// gates) x 32 batch rows of direction d; 512 threads = 8 waves, wave w owns k-chunk (w & 3) of
+// the contraction for batch-row half (w >> 2).  16 x ceil(B/32) x 2 <= 256 workgroups at
+// B <= 256, one per CU, all resident (checked by the host against the occupancy query).
+// Every arithmetic step (per-wave MFMA order, 4-way k-chunk reduction order, cell) equals
+// rec_step_kernel's, so both paths give bitwise identical results.
+//
+// Triple-buffered granules: a workgroup writing step s's h into buffer (s+1)%3 has, during step
+// s-1, seen every group member's step s-2 output, hence every member finished reading buffer
+// (s-2)%3 == (s+1)%3.  Successive writes of one buffer are 3 steps apart, so their parity tags
+// differ and a 1-bit tag separates new from old; the initial fill gives each buffer the parity
+// its first reader does NOT expect (reset_rec_layer).  Every cell writes its word every step
+// (0 for inactive and padding rows) so no wait depends on lengths.  Spins are bounded (~2 s of
+// s_memrealtime and a pass count); a timeout sets CASR_DEV_REC_TIMEOUT and the workgroup leaves
+// the loop.
+#include "casr_common.h"
+#include "casr_internal.h"
+
+namespace casr {
+
+namespace {
+
+constexpr int RG = 32;                 // batch rows per workgroup
+constexpr int NKC = H / 64;            // 4 k-chunks of 64 hidden units
+constexpr uint64_t SPIN_TICKS = 200000000ull;  // s_memrealtime runs at 100 MHz: 2 s
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t TAG_BIT = 0x40000000u;
+constexpr uint32_t NONFINITE = 0x3FFFFFFFu;
+
+CASR_DEV void store_granule(uint32_t* p, int step_tagged, float v) {
+  uint32_t x = __float_as_uint(v);
+  if (!(fabsf(v) < 2.0f)) x = NONFINITE;
+  x |= (step_tagged & 1) ? TAG_BIT : 0u;
+  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dword sc1
+}
+
+CASR_DEV float decode_granule(uint32_t x) {
+  x &= ~TAG_BIT;
+  return (x & 0x7FFFFFFFu) == NONFINITE ? __uint_as_float(0x7FC00000u) : __uint_as_float(x);
+}
+
+__global__ __launch_bounds__(512, 2) void rec_layer_kernel(
+    const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
+    float* __restrict__ out, uint32_t* __restrict__ hx, float* __restrict__ hfin,
+    float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
+    int32_t* __restrict__ err, uint32_t* __restrict__ trace) {
+  __shared__ f32x4 red[2][8][4][64];  // double-buffered k-chunk partials (64 KB)
+  __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
+  const int ub = blockIdx.x, rg = blockIdx.y, d = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kc = w & 3, half = w >> 2;
+  const size_t plane = (size_t)Bp * H;  // granules per direction per buffer
+
+  // ---- epilogue cell of this thread: batch row rl (of 32), unit u (of 16)
+  const int rl = tid >> 4, u = tid & 15;
+  const int b = rg * RG + rl;
+  const int len = b < B ? min(max(lens[b], 0), Tp) : 0;
+  const int U = ub * 16 + u;
+  const size_t si = ((size_t)d * B + b) * H + U;       // hfin / cst index (valid when b < B)
+  const size_t gi = ((size_t)d * Bp + b) * H + U;      // granule index within a buffer
+  if (tid == 0) {
+    s_tmax = 0;
+    s_quit[0] = s_quit[1] = 0;
+  }
+  __syncthreads();
+  if (u == 0 && len > 0) atomicMax(&s_tmax, len);
+
+  // ---- this wave's W_hh fragments, resident for the whole layer (64 VGPRs)
+  const float* Wd = Whh_f + (size_t)d * (H / 16) * 4 * NKC * FRAG;
+  float4 bw[4][4];
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) {
+    const float* wb = Wd + ((size_t)(ub * 4 + tn) * NKC + kc) * FRAG + lane * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bw[tn][q] = *reinterpret_cast<const float4*>(wb + q * 256);
+  }
+  // granule sweep of this wave: rows (lane & 15) of its half, units kc*64 + (lane>>4)*16 + 0..15;
+  // the buffer descriptor takes the wave-uniform part, the lane part is the byte voffset
+  const int wbase = __builtin_amdgcn_readfirstlane(((d * Bp + rg * RG + half * 16) * H + kc * 64));
+  const int voff = ((lane & 15) * H + (lane >> 4) * 16) * (int)sizeof(uint32_t);
+  __syncthreads();
+  const int tmax = s_tmax;
+
+  float c = 0.f;
+  // epilogue operands that do not depend on h (Gin gates, residual input) are software-pipelined
+  // one step ahead: step s+1's are issued right after step s's granule sweep, so they land
+  // during the MFMAs / cell instead of in front of the next sweep's vmcnt(0) wait
+  float gin_v[4] = {0.f, 0.f, 0.f, 0.f}, x_res = 0.f;
+  auto load_operands = [&](int s, float (&g)[4], float& xr) {
+    if (s < len) {
+      const int t = (d == 0) ? s : (len - 1 - s);
+      const float* gp = Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + ub * 64;
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) g[tn] = gp[tn * 16 + u];
+      if (residual) xr = xin[((size_t)b * Tp + t) * C + d * H + U];
+    }
+  };
+  load_operands(0, gin_v, x_res);
+  uint32_t* tr = trace ? trace + ((size_t)((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + w) * Tp * 5 : nullptr;
+  for (int s = 0; s < tmax; ++s) {
+    const bool act = s < len;
+    uint32_t npass = 0;
+    if (tr && lane == 0) tr[s * 5 + 0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    f32x4 acc[4];
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) acc[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float gin_n[4] = {0.f, 0.f, 0.f, 0.f}, x_n = 0.f;
+    if (s > 0) {
+      // h_{s-1}: words tagged with the parity of s in buffer s % 3
+      uint32_t* src = hx + (size_t)(s % 3) * 2 * plane + wbase;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(src, 0, 16 * H * (int)sizeof(uint32_t), 0x00020000);
+      const uint32_t want = (s & 1) ? TAG_BIT : 0u;
+      u32x4 v[4];
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (uint32_t pass = 0;; ++pass) {
+        asm volatile("" ::: "memory");
+        uint32_t bad = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + i * 16, 0, 16 /* sc1 */);
+          bad |= (v[i].x ^ want) | (v[i].y ^ want) | (v[i].z ^ want) | (v[i].w ^ want);
+        }
+        const bool ok = (bad & TAG_BIT) == 0;
+        npass = pass + 1;
+        if (__all(ok)) break;
+        // two independent bounds: wall clock, and a pass count (each pass >= one sc1 round trip)
+        if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || pass > (1u << 22)) {
+          if (lane == 0) {
+            s_quit[s & 1] = 1;
+            __hip_atomic_fetch_or(err, CASR_DEV_REC_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (tr && lane == 0) tr[s * 5 + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+      load_operands(s + 1, gin_n, x_n);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float a0 = decode_granule(v[q].x), a1 = decode_granule(v[q].y);
+        const float a2 = decode_granule(v[q].z), a3 = decode_granule(v[q].w);
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) {
+          acc[tn] = mfma16x16x4(a0, bw[tn][q].x, acc[tn]);
+          acc[tn] = mfma16x16x4(a1, bw[tn][q].y, acc[tn]);
+          acc[tn] = mfma16x16x4(a2, bw[tn][q].z, acc[tn]);
+          acc[tn] = mfma16x16x4(a3, bw[tn][q].w, acc[tn]);
+        }
+      }
+    } else {
+      load_operands(1, gin_n, x_n);
+    }
+    f32x4 (*rb)[4][64] = red[s & 1];
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) rb[w][tn][lane] = acc[tn];
+    __syncthreads();
+    if (s_quit[s & 1]) break;
+    if (tr && lane == 0) tr[s * 5 + 2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+
+    // cell (same reduction order as rec_step_kernel: k-chunks 0..3, then + Gin)
+    const int hw = (rl >> 4) * 4, rr = rl & 15;
+    const int src_lane = u + 16 * (rr >> 2), reg = rr & 3;
+    float h2 = 0.f;
+    if (act) {
+      float gate[4];
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) {
+        float sum = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) sum += rb[hw + ww][tn][src_lane][reg];
+        gate[tn] = sum + gin_v[tn];
+      }
+      float c2;
+      lstm_cell(gate[0], gate[1], gate[2], gate[3], c, h2, c2);
+      c = c2;
+      const int t = (d == 0) ? s : (len - 1 - s);
+      const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
+      if (s == len - 1) hfin[si] = h2;
+      out[oi] = residual ? (h2 + x_res) : h2;
+    }
+    if (s + 1 < tmax) store_granule(hx + (size_t)((s + 1) % 3) * 2 * plane + gi, s + 1, h2);
+    if (tr && lane == 0) {
+      tr[s * 5 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+      tr[s * 5 + 4] = npass;
+    }
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) gin_v[tn] = gin_n[tn];
+    x_res = x_n;
+  }
+  if (b < B) cst[si] = c;
+}
+
+}  // namespace
+
+size_t rec_layer_granule_bytes(int B) {
+  const int Bp = (B + RG - 1) / RG * RG;
+  return (size_t)3 * 2 * Bp * H * sizeof(uint32_t);
+}
+
+int rec_layer_grid_blocks(int B) { return (H / 16) * ((B + RG - 1) / RG) * 2; }
+
+hipError_t rec_layer_occupancy(int* blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rec_layer_kernel, 512, 0);
+}
+
+hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
+  // Guideline 16: re-initialise every call.  Buffer j is first read at step j (j = 1, 2) or 3
+  // (j = 0), expecting parity 1, 0, 1: fill buffers 0 and 1 with parity 0, buffer 2 with 1.
+  const size_t per = rec_layer_granule_bytes(B) / 4 / 3;
+  hipError_t e = fill_u32(hx, 0u, 2 * per, s);
+  return e == hipSuccess ? fill_u32(hx + 2 * per, TAG_BIT, per, s) : e;
+}
+
+hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
+                            uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
+                            int residual, int32_t* err, uint32_t* trace, hipStream_t s) {
+  const int Bp = (B + RG - 1) / RG * RG;
+  dim3 grid(H / 16, Bp / RG, 2);
+  hipLaunchKernelGGL(rec_layer_kernel, grid, dim3(512), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens,
+                     B, Bp, Tp, residual, err, trace);
+  return hipGetLastError();
+}
+
+}  // namespace casr

@@ -141,11 +141,22 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
 int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uint8_t* rec_valid,
                       void* stream);
 
-/* Guard bits raised by the decode kernels since the last casr_greedy / casr_beam (0 = clean):
- * a data-dependent index out of range (1 token, 2 predecessor row, 4 NaN logit row, 8 beam
- * candidate, 16 back-pointer) is clamped and reported here instead of faulting the device.
- * Synchronises `stream`. */
+/* Guard bits raised by the device since the last casr_encode / casr_greedy / casr_beam
+ * (0 = clean): a data-dependent index out of range (1 token, 2 predecessor row, 4 NaN logit
+ * row, 8 beam candidate, 16 back-pointer) is clamped and reported here instead of faulting
+ * the device; 32 = a bounded hand-off wait of the persistent recurrence expired (results of
+ * that casr_encode are invalid).  Synchronises `stream`. */
 int casr_device_flags(casr_handle* h, int32_t* flags_host, void* stream);
+
+/* Encoder recurrence strategy.  Default (enable = 1): one persistent launch per layer runs all
+ * Tp steps, workgroups keep W_hh and c in registers and exchange h through tagged
+ * write-through granules; used when its grid (16 x ceil(B/32) x 2 workgroups of 512 threads)
+ * fits the device's resident capacity, else the per-step launches below.  0 = per-step
+ * launches always.  Both give bitwise identical results. */
+int casr_set_persistent(casr_handle* h, int enable);
+
+/* Which recurrence casr_encode would use for batch B: 1 persistent, 0 per-step, -1 bad args. */
+int casr_recurrence_mode(const casr_handle* h, int B);
 
 /* The launch-bound loops (each layer's Tp recurrence steps, the whole decode loop) are
  * captured once per shape into hipGraphs on a private stream and replayed on `stream`

@@ -179,6 +179,61 @@ def test_graph_replay_equals_eager(eng):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B", [37, 256])
+def test_persistent_recurrence_equals_per_step(eng, B):
+    """The persistent per-layer recurrence (granule hand-offs) and the per-step launches give
+    bitwise-identical encoder outputs and final states, on ragged lengths (B = 37: a partial
+    32-row group and padding rows; B = 256: the full 256-workgroup grid)."""
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    rs = np.random.RandomState(11)
+    frames = rs.randint(9, 801, size=B)
+    frames[0], frames[-1] = 800, 9  # longest and shortest (T' = 3)
+    x = np.zeros((B, 800, 80), np.float32)
+    for b in range(B):
+        x[b, :frames[b]] = fbank_for(b, int(frames[b]))
+    feat, flen = eng.features(torch.from_numpy(x).to(eng.device),
+                              torch.from_numpy(frames.astype(np.int32)).to(eng.device))
+    assert eng.recurrence_mode(B) == 1, "B <= 256 must take the persistent path on MI355X"
+    outs = []
+    for persistent in (False, True, True):
+        eng.set_persistent(persistent)
+        eng.encode(feat, flen)
+        assert eng.device_flags() == 0
+        outs.append([t.cpu() for t in eng.encoder_results()])
+    eng.set_persistent(True)
+    for ref, got in ((outs[0], outs[1]), (outs[1], outs[2])):
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b)
+
+
+def test_persistent_recurrence_nan_row_isolated(eng):
+    """A T' = 1 utterance has NaN features (unbiased std of one frame, main.py:37, as in the
+    reference).  Its NaN h must travel through the tagged hand-off (non-finite code) without
+    stalling the other workgroups, and every other row must be bitwise unaffected."""
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    B, T = 40, 240
+    frames = np.full(B, T, np.int32)
+    x = np.stack([fbank_for(b, T) for b in range(B)])
+    fb = torch.from_numpy(x).to(eng.device)
+    eng.set_persistent(True)
+    feat, flen = eng.features(fb, torch.from_numpy(frames).to(eng.device))
+    eng.encode(feat, flen)
+    assert eng.device_flags() == 0
+    clean = [t.cpu() for t in eng.encoder_results()]
+    frames[5] = 3  # T' = 1
+    feat, flen = eng.features(fb, torch.from_numpy(frames).to(eng.device))
+    assert torch.isnan(feat[5, 0]).all()
+    eng.encode(feat, flen)
+    assert eng.device_flags() == 0, "a NaN row must not stall the persistent recurrence"
+    enc, h, c, keys = [t.cpu() for t in eng.encoder_results()]
+    keep = [b for b in range(B) if b != 5]
+    for a, b_ in zip(clean, (enc, h, c, keys)):
+        assert torch.equal(a[keep], b_[keep])
+    assert torch.isnan(enc[5, 0]).all() and (enc[5, 1:] == 0).all()
+
+
 def _bench_batch(eng, B, T=800):
     x = np.stack([fbank_for(b, T) for b in range(B)])
     fb = torch.from_numpy(x).to(eng.device)
