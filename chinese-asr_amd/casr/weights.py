@@ -111,8 +111,8 @@ def load_checkpoint(path):
     """Read a reference ``.ckpt`` (model.py:357-370) without executing pickled code.
 
     ``torch.load(weights_only=True)`` refuses arbitrary classes, which the reference's
-    ``args`` entry (a pickled ``TrainVar``, util.py:2356) may be; in that case the
-    tensors are still returned and ``args`` is reported as ``None``.
+    ``args`` entry (a pickled ``TrainVar``, util.py:2356) may be; such a file is refused
+    with a RuntimeError naming the remedy (nothing from it is executed).
     Returns ``(enc_sd, dec_sd, args)``."""
     import torch
     try:

@@ -35,7 +35,11 @@ for s in $STAGES; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
         python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS} > $OUT/prof_bench.json 2> $OUT/prof.err
       rc=$?; tail -3 $OUT/prof.err; stop_on_fault $rc prof $OUT/prof.err
-      find $OUT/prof -name "*kernel_stats.csv" | head -3 ;;
+      python tools/prof_by_grid.py $OUT/prof/run_kernel_trace.csv 30 > $OUT/prof_by_grid.txt 2>&1
+      head -12 $OUT/prof_by_grid.txt ;;
+    trace)
+      timeout -k 10 300 python tools/rec_trace.py > $OUT/rec_trace.txt 2>&1
+      rc=$?; cat $OUT/rec_trace.txt; stop_on_fault $rc trace $OUT/rec_trace.txt ;;
   esac
 done
 echo "session done"
