@@ -34,9 +34,11 @@ class Engine:
         self.handle = ctypes.c_void_p()
         c = _lib.config_struct(cfg)
         _lib.check(self.lib.casr_create(ctypes.byref(c), self.device.index, ctypes.byref(self.handle)))
-        if packed is None:
+        self.packed = None
+        if packed is None and enc_sd is not None:
             packed = _lib.pack_weights(cfg, enc_sd, dec_sd)
-        self.bind(packed)
+        if packed is not None:  # no weights: front-end only (log_mel / features)
+            self.bind(packed)
         self._B = self._Tp = None
 
     def bind(self, packed):
@@ -60,9 +62,23 @@ class Engine:
             pass
 
     # ------------------------------------------------------------------ features
+    def log_mel(self, wav, n_samples, t_max=None, preemphasis=0.97):
+        """wav [B, n_max] float32 (device), n_samples [B] int (device or host) ->
+        (fbank [B, t_max, 80] log-mel, frames [B] int32).  get_log_mel data.py:167-224."""
+        wav = wav.to(self.device, torch.float32).contiguous()
+        B, n_max = wav.shape
+        ns = torch.as_tensor(n_samples).to(self.device, torch.int32).contiguous()
+        t_max = _lib.log_mel_frames(n_max) if t_max is None else int(t_max)
+        fbank = torch.empty(B, max(t_max, 1), self.cfg.n_mels, device=self.device, dtype=torch.float32)
+        frames = torch.empty(B, device=self.device, dtype=torch.int32)
+        _lib.check(self.lib.casr_log_mel(self.handle, _ptr(wav), _ptr(ns), B, n_max, max(t_max, 1),
+                                         ctypes.c_float(preemphasis), _ptr(fbank), _ptr(frames), _stream()),
+                   self.handle)
+        return fbank, frames
+
     def features(self, fbank, frames, eps=1e-6):
         """fbank [B, T, n_mels] float32 (device), frames [B] int32 (device) ->
-        (feat [B, T//3, feat_dim], feat_len [B] int32)."""
+        (feat [B, T//3, feat_dim], feat_len [B] int32).  eps < 0: no CMVN."""
         fbank = fbank.contiguous()
         B, T, _ = fbank.shape
         feat = torch.empty(B, T // 3, self.cfg.feat_dim, device=self.device, dtype=torch.float32)

@@ -20,7 +20,8 @@ EXPORTS = [
     "casr_bind_weights", "casr_destroy", "casr_last_error", "casr_features",
     "casr_gather_utterances", "casr_encode", "casr_encoder_results", "casr_greedy", "casr_beam",
     "casr_beam_records", "casr_profile_enable", "casr_profile_read", "casr_set_graphs",
-    "casr_device_flags", "casr_set_persistent", "casr_recurrence_mode",
+    "casr_device_flags", "casr_set_persistent", "casr_recurrence_mode", "casr_log_mel",
+    "casr_log_mel_frames", "casr_mel_filterbank",
 ]
 
 # kernel classes of casr_profile_enable / casr_profile_read (include/casr.h)
@@ -89,6 +90,9 @@ def load(path=None):
         "casr_device_flags": (i32, [vp, ctypes.POINTER(ctypes.c_int32), vp]),
         "casr_set_persistent": (i32, [vp, i32]),
         "casr_recurrence_mode": (i32, [vp, i32]),
+        "casr_log_mel": (i32, [vp, vp, vp, i32, i32, i32, f32, vp, vp, vp]),
+        "casr_log_mel_frames": (i32, [i32]),
+        "casr_mel_filterbank": (i32, [i32, f32, f32, i32, vp]),
         "casr_profile_read": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
@@ -105,6 +109,21 @@ def check(rc, handle=None):
     if rc != 0:
         msg = load().casr_last_error(handle)
         raise CasrError(f"{STATUS.get(rc, rc)}: {msg.decode(errors='replace') if msg else ''}")
+
+
+def mel_filterbank(n_stft=257, f_min=80.0, f_max=7600.0, n_mels=80):
+    """The filterbank casr_log_mel uses (create_fb_matrix, data.py:21-57), computed by the
+    library on the host: float32 [n_stft, n_mels]."""
+    lib = load()
+    out = np.empty((n_stft, n_mels), np.float32)
+    check(lib.casr_mel_filterbank(n_stft, ctypes.c_float(f_min), ctypes.c_float(f_max), n_mels,
+                                  out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+def log_mel_frames(n_samples):
+    """Frames of log-mel an utterance of n_samples produces (0 below 513 samples)."""
+    return int(load().casr_log_mel_frames(int(n_samples)))
 
 
 def config_struct(cfg):

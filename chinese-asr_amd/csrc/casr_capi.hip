@@ -105,6 +105,8 @@ struct casr_handle {
   DevBuf gin, out0, out1, hbuf, cst, hfin, keysT, lens;
   DevBuf hx;       // persistent recurrence: tagged h words [3][2][Bp][H]
   DevBuf eflag;    // encoder device guard bits (CASR_DEV_REC_TIMEOUT)
+  DevBuf fe_const; // FrontendConst (filterbank, window, twiddles), built on first casr_log_mel
+  DevBuf fflag;    // front-end device guard bits (CASR_DEV_BAD_AUDIO)
   bool use_persistent = true;
   int rec_capacity = 0;  // workgroups of rec_layer_kernel resident at once (CUs x blocks/CU)
   int B = 0, Tp = 0;
@@ -323,7 +325,7 @@ void casr_destroy(casr_handle* h) {
     if (h->ev_out[i]) (void)hipEventDestroy(h->ev_out[i]);
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
-  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->hx, &h->eflag,
+  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->hx, &h->eflag, &h->fe_const, &h->fflag,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout})
     b->release();
   delete h;
@@ -355,6 +357,39 @@ int casr_features(casr_handle* h, const float* fbank, const int32_t* frames, int
   HIP_OK(h, hipSetDevice(h->device));
   ProfScope ps(&h->prof, CASR_K_FEATURES, (hipStream_t)stream);
   HIP_OK(h, launch_features(fbank, frames, B, T, eps, feat, feat_len, (hipStream_t)stream));
+  return CASR_OK;
+}
+
+int casr_log_mel_frames(int n_samples) { return frontend_frames(n_samples); }
+
+int casr_mel_filterbank(int n_stft, float f_min, float f_max, int n_mels, float* fb_host) {
+  if (n_stft < 2 || n_mels < 1 || !fb_host || !(f_max > f_min))
+    return fail(nullptr, CASR_ERR_ARG, "casr_mel_filterbank: bad arguments");
+  mel_filterbank(n_stft, f_min, f_max, n_mels, fb_host);
+  return CASR_OK;
+}
+
+int casr_log_mel(casr_handle* h, const float* wav, const int32_t* n_samples, int B, int n_max, int t_max,
+                 float preemphasis, float* fbank, int32_t* frames, void* stream) {
+  if (!h || !wav || !n_samples || !fbank || !frames || B <= 0 || n_max <= 0 || t_max <= 0)
+    return fail(h, CASR_ERR_ARG, "casr_log_mel: bad arguments");
+  if (t_max < frontend_frames(n_max))
+    return fail(h, CASR_ERR_ARG, "casr_log_mel: t_max %d < %d frames of n_max %d samples", t_max,
+                frontend_frames(n_max), n_max);
+  if ((size_t)n_max * B > (size_t)1 << 40) return fail(h, CASR_ERR_ARG, "casr_log_mel: batch too large");
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  if (!h->fe_const.p) {
+    FrontendConst c;
+    build_frontend_const(&c);
+    HIP_OK(h, h->fe_const.ensure(sizeof(FrontendConst)));
+    HIP_OK(h, hipMemcpy(h->fe_const.p, &c, sizeof c, hipMemcpyHostToDevice));
+  }
+  HIP_OK(h, h->fflag.ensure(16));
+  HIP_OK(h, hipMemsetAsync(h->fflag.p, 0, 16, s));
+  ProfScope ps(&h->prof, CASR_K_FEATURES, s);
+  HIP_OK(h, launch_log_mel(wav, n_samples, B, n_max, t_max, preemphasis, h->fe_const.as<FrontendConst>(), fbank,
+                           frames, h->fflag.as<int32_t>(), s));
   return CASR_OK;
 }
 
@@ -667,11 +702,12 @@ int casr_device_flags(casr_handle* h, int32_t* flags, void* stream) {
   *flags = 0;
   HIP_OK(h, hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
-  int32_t dec = 0, enc = 0;
+  int32_t dec = 0, enc = 0, fe = 0;
   if (h->d.err) HIP_OK(h, hipMemcpyAsync(&dec, h->d.err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   if (h->eflag.p) HIP_OK(h, hipMemcpyAsync(&enc, h->eflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (h->fflag.p) HIP_OK(h, hipMemcpyAsync(&fe, h->fflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_OK(h, hipStreamSynchronize(s));
-  *flags = dec | enc;
+  *flags = dec | enc | fe;
   return CASR_OK;
 }
 

@@ -32,6 +32,7 @@ constexpr int CASR_DEV_NAN_LOGITS = 4;   // no finite maximum in a logit row (gr
 constexpr int CASR_DEV_BAD_CAND = 8;     // beam candidate index not in [0, k*V)
 constexpr int CASR_DEV_BAD_BACKPTR = 16; // back-pointer walk left [0, k)
 constexpr int CASR_DEV_REC_TIMEOUT = 32; // persistent recurrence: a bounded hand-off wait expired
+constexpr int CASR_DEV_BAD_AUDIO = 64;   // front-end: n_samples < 513 (torch.stft raises) or > n_max
 
 // MFMA-fragment-major weight block: a 16-row x 64-k tile stored as [q=0..3][lane][4] so
 // lane l reads row (l&15), k = 16*(l>>4) + 4q + e with one coalesced 16 B load per q.
@@ -140,6 +141,20 @@ struct GraphCache {
 // fill.hip (graph-safe replacements for hipMemsetAsync)
 hipError_t fill_u32(void* p, uint32_t v, size_t n_words, hipStream_t s);
 hipError_t fill_u8(void* p, uint8_t v, size_t n_bytes, hipStream_t s);
+
+// frontend.hip: wav -> log-mel.  Constant tables live in one device struct per handle.
+struct FrontendConst {
+  float fb[257 * F];            // [bin][mel]
+  int32_t lo[F], hi[F];         // nonzero bin range of each mel filter
+  float win[400];               // periodic hann(400)
+  double tw256r[128], tw256i[128];  // exp(-2 pi i k / 256)
+  double tw512r[257], tw512i[257];  // exp(-2 pi i q / 512)
+};
+void mel_filterbank(int n_stft, float f_min, float f_max, int n_mels, float* fb);
+void build_frontend_const(FrontendConst* c);
+int frontend_frames(int n_samples);
+hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nmax, int Tmax, float pre,
+                          const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s);
 
 // features.hip
 hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int T, float eps,

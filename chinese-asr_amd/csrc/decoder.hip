@@ -37,12 +37,26 @@ struct RedTile {
   }
 };
 
+// Grid: 1-D, XCD-aware.  Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
+// "Workgroup dispatch": speed only, never correctness), so linear id L runs on XCD L % 8.  All
+// NR row blocks of one 64-column weight slice get ids with the same L % 8: the slice is
+// fetched into one XCD's L2 once and re-read from there by every row block.
+__device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
+  const int L = blockIdx.x, x = L & 7, j = L >> 3;
+  nb = (j / NR) * 8 + x;
+  rb = j % NR;
+  return nb < NB;
+}
+
+inline unsigned xcd_grid(int NB, int NR) { return (unsigned)(8 * ((NB + 7) / 8) * NR); }
+
 template <int TM, class ASrc, class Epi>
-__global__ __launch_bounds__(256) void rowgemm_kernel(int nkc, const float* __restrict__ Wf,
+__global__ __launch_bounds__(256) void rowgemm_kernel(int NB, int NR, int nkc, const float* __restrict__ Wf,
                                                       ASrc asrc, Epi epi) {
   __shared__ RedTile<TM> red;
   if (epi.skip()) return;
-  const int nb = blockIdx.x, rb = blockIdx.y;
+  int nb, rb;
+  if (!xcd_tile(NB, NR, nb, rb)) return;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
 
@@ -603,9 +617,9 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
     constexpr int TM = 1;
     DecLstmA asrc{a.W + a.L.emb, st_old, d.tok[l & 1], d.src[l & 1], d.err, R, a.V};
     DecLstmEpi<TM> epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, R, l, total};
-    dim3 grid(HD / 16, (R + 16 * TM - 1) / (16 * TM));
-    hipLaunchKernelGGL((rowgemm_kernel<TM, DecLstmA, DecLstmEpi<TM>>), grid, dim3(256), 0, s,
-                       KDEC / 64, a.W + a.L.dec_w, asrc, epi);
+    const int NB = HD / 16, NR = (R + 16 * TM - 1) / (16 * TM);
+    hipLaunchKernelGGL((rowgemm_kernel<TM, DecLstmA, DecLstmEpi<TM>>), dim3(xcd_grid(NB, NR)), dim3(256),
+                       0, s, NB, NR, KDEC / 64, a.W + a.L.dec_w, asrc, epi);
   }
   hipError_t e;
   {
@@ -618,9 +632,9 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
     constexpr int TM = 2;
     ProjA asrc{st_new, R};
     ProjEpi<TM> epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total};
-    dim3 grid(a.L.VP / 64, (R + 16 * TM - 1) / (16 * TM));
-    hipLaunchKernelGGL((rowgemm_kernel<TM, ProjA, ProjEpi<TM>>), grid, dim3(256), 0, s, KPROJ / 64,
-                       a.W + a.L.proj_w, asrc, epi);
+    const int NB = a.L.VP / 64, NR = (R + 16 * TM - 1) / (16 * TM);
+    hipLaunchKernelGGL((rowgemm_kernel<TM, ProjA, ProjEpi<TM>>), dim3(xcd_grid(NB, NR)), dim3(256), 0, s,
+                       NB, NR, KPROJ / 64, a.W + a.L.proj_w, asrc, epi);
   }
   return hipGetLastError();
 }

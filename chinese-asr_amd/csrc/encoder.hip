@@ -44,16 +44,42 @@ struct KeysEpi {  // keysT[b][a][t] = acc + b_attn[a], row = b*Tp + t, row strid
   }
 };
 
+// XCD-aware tile order (speed only: MI355X_MICROARCH.md "Workgroup dispatch" — workgroups are
+// dealt round-robin over the 8 XCDs, each with its own 4 MiB L2).  The NB column blocks are split
+// into NG groups; XCD x works on group x % NG and on every (8/NG)-th row block, walking all the
+// group's column blocks of one row block back to back.  Each XCD's L2 then holds 1/NG of W and
+// each A row block is fetched by NG XCDs instead of all 8.
+struct TileOrder {
+  int NB, NM, NG;
+  __host__ __device__ int blocks() const { return 8 * (NB / NG) * ((NM + 8 / NG - 1) / (8 / NG)); }
+  __device__ bool tile(int L, int& n, int& m) const {
+    const int x = L & 7, j = L >> 3, nbg = NB / NG;
+    n = (x % NG) * nbg + (j % nbg);
+    m = (j / nbg) * (8 / NG) + (x / NG);
+    return m < NM;
+  }
+};
+
+inline TileOrder tile_order(int NB, int NM, int K) {
+  // smallest group count whose W share (NB/NG blocks of 128 rows x K) fits 3/4 of an L2
+  // (input projection: NG = 2, 2.9 MB at K = 720)
+  int NG = 1;
+  while (NG < 8 && NB % (NG * 2) == 0 && (size_t)(NB / NG) * GB_N * K * 4 > (3u << 20)) NG *= 2;
+  return TileOrder{NB, NM, NG};
+}
+
 template <class Epi>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ Amat, int lda,
                                                       const float* __restrict__ Wmat, int ldw,
-                                                      int M, int N, int K, Epi epi) {
+                                                      int M, int N, int K, TileOrder order, Epi epi) {
   __shared__ __attribute__((aligned(16))) float smem[2 * (GB_M + GB_N) * GB_LDK];
   constexpr int STAGE = (GB_M + GB_N) * GB_LDK;  // one buffer: A tile then W tile
 
+  int nt, mt;
+  if (!order.tile(blockIdx.x, nt, mt)) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * GB_M, n0 = blockIdx.x * GB_N;
+  const int m0 = mt * GB_M, n0 = nt * GB_N;
   const int r = lane & 15, g = lane >> 4;
 
   f32x4 acc[4][4];
@@ -135,9 +161,9 @@ hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, con
                              float* Gin, hipStream_t s) {
   const int N = 8 * H;
   StoreBiasEpi epi{Gin, bias, N};
-  dim3 grid(N / GB_N, (M + GB_M - 1) / GB_M);
-  hipLaunchKernelGGL(gemm_nt_kernel<StoreBiasEpi>, grid, dim3(256), 0, s, X, Din, W, Din, M, N,
-                     Din, epi);
+  const TileOrder order = tile_order(N / GB_N, (M + GB_M - 1) / GB_M, Din);
+  hipLaunchKernelGGL(gemm_nt_kernel<StoreBiasEpi>, dim3(order.blocks()), dim3(256), 0, s, X, Din, W,
+                     Din, M, N, Din, order, epi);
   return hipGetLastError();
 }
 
@@ -145,9 +171,9 @@ hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, cons
                        float* keysT, hipStream_t s) {
   const int M = B * Tp;
   KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3};
-  dim3 grid(A / GB_N, (M + GB_M - 1) / GB_M);
-  hipLaunchKernelGGL(gemm_nt_kernel<KeysEpi>, grid, dim3(256), 0, s, enc, C, wencT, C, M, A, C,
-                     epi);
+  const TileOrder order = tile_order(A / GB_N, (M + GB_M - 1) / GB_M, C);
+  hipLaunchKernelGGL(gemm_nt_kernel<KeysEpi>, dim3(order.blocks()), dim3(256), 0, s, enc, C, wencT,
+                     C, M, A, C, order, epi);
   return hipGetLastError();
 }
 

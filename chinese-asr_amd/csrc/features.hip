@@ -125,8 +125,9 @@ hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int
   if (Tp <= 0 || B <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(stack_kernel, dim3(Tp, B), dim3(256), 0, s, fbank, frames, T, Tp, feat,
                      feat_len);
-  hipLaunchKernelGGL(cmvn_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, feat, feat_len, Tp,
-                     eps);
+  // eps < 0: no CMVN (the stacked features get_log_mel returns, data.py:226-249)
+  if (eps >= 0.f)
+    hipLaunchKernelGGL(cmvn_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, feat, feat_len, Tp, eps);
   return hipGetLastError();
 }
 

@@ -98,9 +98,30 @@ const char* casr_last_error(const casr_handle* h); /* h may be NULL: last global
  * 3-frame stacking to feat_dim, per-utterance per-dimension (x-mean)/(std_unbiased+eps).
  *   fbank    [B][T][n_mels]    frames [B] (valid frames per utterance, <= T)
  *   feat     [B][Tp][feat_dim] with Tp = T/3; rows past frames[b]/3 are zero
- *   feat_len [B] = frames[b]/3 */
+ *   feat_len [B] = frames[b]/3
+ * eps < 0 skips CMVN (the stacked features get_log_mel itself returns). */
 int casr_features(casr_handle* h, const float* fbank, const int32_t* frames, int B, int T,
                   float eps, float* feat, int32_t* feat_len, void* stream);
+
+/* wav -> log-mel (get_log_mel data.py:167-224, inference: no dither / augmentation):
+ * pre-emphasis (data.py:201-202), |STFT|^2 with n_fft 512, hop 160, periodic hann(400)
+ * centred, center=False (data.py:205-221), mel filterbank (MelScale, create_fb_matrix
+ * data.py:21-106, incl. the linspace(80, 7600, 257) bin quirk), eps floor and log
+ * (data.py:223-224).
+ *   wav       [B][n_max] float32 samples (soundfile float32 scale), n_samples [B] int32
+ *   fbank     [B][t_max][80] log-mel, rows past frames[b] zero
+ *   frames    [B] = 1 + (n_samples[b] - 1 - 512) / 160  (0 and device flag 64 when
+ *             n_samples[b] < 513, where torch.stft raises, data.py:204)
+ * t_max must be >= casr_log_mel_frames(n_max). */
+int casr_log_mel(casr_handle* h, const float* wav, const int32_t* n_samples, int B, int n_max, int t_max,
+                 float preemphasis, float* fbank, int32_t* frames, void* stream);
+
+/* Frames casr_log_mel produces for an utterance of n samples (0 if n < 513).  Host only. */
+int casr_log_mel_frames(int n_samples);
+
+/* The mel filterbank [n_stft][n_mels] casr_log_mel uses (create_fb_matrix, data.py:21-57,
+ * float32).  Host only, no device needed. */
+int casr_mel_filterbank(int n_stft, float f_min, float f_max, int n_mels, float* fb_host);
 
 /* The list-of-tensors boundary of Model.eval_one_batch_* (model.py:514-516): gather B
  * device rows [lens[b]][feat_dim] (utt_ptrs is a DEVICE array of B device pointers) into
@@ -145,7 +166,8 @@ int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uin
  * (0 = clean): a data-dependent index out of range (1 token, 2 predecessor row, 4 NaN logit
  * row, 8 beam candidate, 16 back-pointer) is clamped and reported here instead of faulting
  * the device; 32 = a bounded hand-off wait of the persistent recurrence expired (results of
- * that casr_encode are invalid).  Synchronises `stream`. */
+ * that casr_encode are invalid); 64 = casr_log_mel got an utterance shorter than 513
+ * samples or longer than n_max.  Synchronises `stream`. */
 int casr_device_flags(casr_handle* h, int32_t* flags_host, void* stream);
 
 /* Encoder recurrence strategy.  Default (enable = 1): one persistent launch per layer runs all

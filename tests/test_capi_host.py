@@ -125,3 +125,26 @@ def test_packed_layout_contract():
                                   dec["attn_mechanism.W_enc"].T)
     np.testing.assert_array_equal(blob[lay["emb"]:lay["emb"] + CFG.vocab * 256].reshape(CFG.vocab, 256),
                                   dec["embedding.weight"])
+
+
+def test_mel_filterbank_matches_reference_fixture():
+    """The library's own create_fb_matrix (data.py:21-57, float32, linspace(80, 7600, 257) bin
+    quirk) against the matrix captured from the reference and against the oracle."""
+    from golden_util import load_golden
+    from oracle import casr_oracle as O
+    G, _ = load_golden()
+    fb = L.mel_filterbank()
+    assert fb.shape == (257, 80)
+    # float32 log10f / powf vs torch's float kernels: <= 1e-5 on weights <= 1 (same bound as the
+    # oracle's own fixture test, tests/test_oracle_golden.py)
+    np.testing.assert_allclose(fb, G["fb_matrix"], atol=2e-5, rtol=0)
+    np.testing.assert_allclose(fb, O.create_fb_matrix(), atol=2e-5, rtol=0)
+    assert ((fb > 0) == (G["fb_matrix"] > 0)).all()  # same filter supports
+
+
+@pytest.mark.parametrize("n", [0, 100, 512, 513, 514, 672, 673, 24000, 128353, 10 ** 6])
+def test_log_mel_frame_count(n):
+    """torch.stft center=False on the pre-emphasised signal (n - 1 samples): 1 + (n-1-512)//160,
+    and the reference raises below 513 samples (data.py:204) -> 0 here (plus a device flag)."""
+    want = 1 + (n - 1 - 512) // 160 if n - 1 >= 512 else 0
+    assert L.log_mel_frames(n) == want

@@ -1,0 +1,82 @@
+"""Per-kernel PMC summary from rocprofv3 --pmc passes (tools/probes/pmc_passes.sh).
+
+Groups dispatches by (kernel, grid size) and prints per-dispatch averages plus derived figures:
+  clock   = GRBM_GUI_ACTIVE / 8 / duration (GRBM sums the 8 XCDs; MI355X_MICROARCH.md DVFS note)
+  mfma%   = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)
+  wait%, stall%, active% = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES
+  fetch   = 2 x FETCH_SIZE (gfx950 tallies 128-B requests at 64 B: MICROARCH §HBM), write = WRITE_SIZE
+With --json, writes {class: hbm_bytes_per_launch} for bench.py's roofline.traffic.
+
+usage: python tools/pmc_summary.py gpurun_out/pmc [--json profiles/pmc_traffic.json]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+CLASS_OF = {  # bench.py kernel classes -> kernel-name prefixes
+    "input_proj": "gemm_nt_kernel<casr::StoreBiasEpi>",
+    "keys": "gemm_nt_kernel<casr::KeysEpi>",
+    "rec_step": "rec_layer_kernel",
+    "dec_lstm": "rowgemm_kernel<1",
+    "proj": "rowgemm_kernel<2",
+    "attention": "attention_kernel",
+    "select": "greedy_select_kernel",
+}
+
+
+def short(name):
+    n = name[:name.index("(")] if "(" in name else name
+    return n.replace("void ", "").replace("casr::", "").replace("(anonymous namespace)::", "")
+
+
+def load(d):
+    per = defaultdict(lambda: defaultdict(list))  # (kernel, grid) -> counter -> [values]
+    dur = defaultdict(dict)
+    for f in glob.glob(os.path.join(d, "*", "*counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            key = (short(r["Kernel_Name"]), int(r["Grid_Size"]))
+            per[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            dur[key][(f, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    return per, dur
+
+
+def main(d, json_out=None):
+    per, dur = load(d)
+    rows = []
+    for key, cs in per.items():
+        avg = {c: sum(v) / len(v) for c, v in cs.items()}
+        us = sum(dur[key].values()) / max(1, len(dur[key]))
+        rows.append((key, avg, us, max(len(v) for v in cs.values())))
+    rows.sort(key=lambda r: -r[2] * r[3])
+    print(f"{'kernel':52s} {'grid':>8s} {'n':>4s} {'us':>8s} {'clkGHz':>6s} {'mfma%':>6s} {'wait%':>6s} {'stall%':>6s} "
+          f"{'lds%':>5s} {'fetchMB':>8s} {'writeMB':>8s}")
+    traffic = {}
+    for (name, grid), a, us, n in rows[:30]:
+        g = a.get("GRBM_GUI_ACTIVE")
+        cyc = g / 8 if g else None
+        clk = cyc / (us * 1e3) if cyc and us else float("nan")
+        mf = 100 * a["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024) if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in a else float("nan")
+        wc = a.get("SQ_WAVE_CYCLES")
+        wait = 100 * a["SQ_WAIT_ANY"] / wc if wc else float("nan")
+        stall = 100 * a["SQ_WAIT_INST_ANY"] / wc if wc else float("nan")
+        lds = 100 * a["SQ_WAIT_INST_LDS"] / wc if wc and "SQ_WAIT_INST_LDS" in a else float("nan")
+        fetch = 2 * a["FETCH_SIZE"] / 1024 if "FETCH_SIZE" in a else float("nan")  # KB -> MB
+        write = a["WRITE_SIZE"] / 1024 if "WRITE_SIZE" in a else float("nan")
+        print(f"{name[:52]:52s} {grid:8d} {n:4d} {us:8.1f} {clk:6.2f} {mf:6.1f} {wait:6.1f} {stall:6.1f} {lds:5.1f} "
+              f"{fetch:8.2f} {write:8.2f}")
+        for cls, pre in CLASS_OF.items():
+            if name.startswith(pre) and cls not in traffic and fetch == fetch:
+                traffic[cls] = {"fetch_bytes": fetch * 1e6 * 1.048576, "write_bytes": write * 1e6 * 1.048576,
+                                "hbm_bytes": (fetch + (write if write == write else 0)) * 1048576.0,
+                                "grid": grid, "note": "per launch, FETCH_SIZE x2 (gfx950) + WRITE_SIZE"}
+    if json_out:
+        json.dump(traffic, open(json_out, "w"), indent=1)
+        print("wrote", json_out)
+
+
+if __name__ == "__main__":
+    a = sys.argv[1:]
+    main(a[0], a[a.index("--json") + 1] if "--json" in a else None)
