@@ -14,7 +14,7 @@
 //      model.py:554-578; beam: top-2k over k*V per utterance with wave shuffles + an LDS
 //      merge and the finished/active rules of model.py:834-929.
 // The GEMMs use v_mfma_f32_16x16x4_f32 (exact fp32) with weights in MFMA-fragment-major
-// order and split-K over the block's 4 waves.  Early exit (model.py:578 / :897-901) is a
+// order, staged by LDS-DMA (dgemm_kernel).  Early exit (model.py:578 / :897-901) is a
 // device-side per-step counter every kernel checks, so the host never synchronises.
 #include <float.h>
 
@@ -23,24 +23,24 @@
 
 namespace casr {
 
-// ------------------------------------------------------------------ split-K row GEMM
-// Block: 16*TM rows x 64 output columns (4 MFMA n-tiles), 4 waves each own every 4th
-// 64-deep k chunk; partial tiles are summed through LDS.
-template <int TM>
-struct RedTile {
-  f32x4 v[4][TM][4][64];
-  __device__ __forceinline__ float get(int rowl, int coll) const {
-    const int tm = rowl >> 4, rl = rowl & 15, tn = coll >> 4, u = coll & 15;
-    const int ln = u + 16 * (rl >> 2), reg = rl & 3;
-    return ((v[0][tm][tn][ln][reg] + v[1][tm][tn][ln][reg]) + v[2][tm][tn][ln][reg]) +
-           v[3][tm][tn][ln][reg];
-  }
-};
-
+// ------------------------------------------------------------------ decode GEMM (LDS-DMA)
+// C[R][N] = A[R][K] . W^T for the decoder LSTMCell (K = 1280, N = 2048 gate rows) and the
+// vocabulary projection (K = 1024, N = 5056).  Block = 64 (or 32) rows x 64 columns, 8 waves:
+// 4 (2) row slabs of 16 x 2 (4) slices of every 64-deep k tile; the slices are added once at the
+// end in a fixed order.  Operand tiles
+// are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4), double-buffered, so the next
+// tile's loads run under the current tile's MFMAs:
+//   * W tile: 4 MFMA-fragment-major blocks (16 rows x 64 k, [q][lane][4]) copied verbatim; a
+//     lane's fragment read is lane-linear, conflict-free;
+//   * A tile: 64 rows x 64 k, 256-B rows, 16-B chunk c of row r at c ^ (r & 15) (XOR on the
+//     per-lane DMA source address, same XOR on the read).  The per-lane source address also
+//     performs the decoder's row gather (embedding row of tok[r], state row of src[r]).
 // Grid: 1-D, XCD-aware.  Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
 // "Workgroup dispatch": speed only, never correctness), so linear id L runs on XCD L % 8.  All
 // NR row blocks of one 64-column weight slice get ids with the same L % 8: the slice is
 // fetched into one XCD's L2 once and re-read from there by every row block.
+constexpr int DG_BK = 64, DG_TILE = 64 * DG_BK;  // W tile: 64 columns x 64 k
+
 __device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
   const int L = blockIdx.x, x = L & 7, j = L >> 3;
   nb = (j / NR) * 8 + x;
@@ -50,76 +50,141 @@ __device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
 
 inline unsigned xcd_grid(int NB, int NR) { return (unsigned)(8 * ((NB + 7) / 8) * NR); }
 
-template <int TM, class ASrc, class Epi>
-__global__ __launch_bounds__(256) void rowgemm_kernel(int NB, int NR, int nkc, const float* __restrict__ Wf,
-                                                      ASrc asrc, Epi epi) {
-  __shared__ RedTile<TM> red;
+__device__ __forceinline__ void lds_dma16(const float* src, float* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// WR row slabs of 16 (block = 16 WR rows x 64 columns), KQ = 8 / WR waves split each 64-deep k
+// tile by MFMA step q (wave kq takes q in [kq * 4/KQ, (kq+1) * 4/KQ)); partials are added in kq order.
+// The two stage buffers are two distinct __shared__ arrays and the k loop is unrolled by 2 so every
+// ds_read names one of them: hipcc then proves the in-flight DMA (into the other array) does not
+// alias the read and does not drain it with vmcnt(0) (one array with a runtime index did: the
+// prefetch was serialised).  Each lane's A source rows are resolved once before the loop (an
+// ordinary load beside in-flight DMA also forces vmcnt(0)).
+template <int WR, class ASrc, class Epi>
+__global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, const float* __restrict__ Wf,
+                                                    ASrc asrc, Epi epi) {
+  constexpr int KQ = 8 / WR, QPW = 4 / KQ, BM = 16 * WR, ATILE = BM * DG_BK;
+  constexpr int NA = BM / 4, NDMA = NA + 16;  // DMA instructions per stage: A (4 rows each) + W
+  constexpr int NSLOT = (NDMA + 7) / 8;      // per wave
+  __shared__ __attribute__((aligned(16))) float buf0[ATILE + DG_TILE];  // [A tile | W tile]
+  __shared__ __attribute__((aligned(16))) float buf1[ATILE + DG_TILE];
   if (epi.skip()) return;
   int nb, rb;
   if (!xcd_tile(NB, NR, nb, rb)) return;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ws = w % WR, kq = w / WR;
   const int r = lane & 15, g = lane >> 4;
 
-  f32x4 acc[TM][4];
+  // per-lane DMA sources that do not depend on k: A row segment bases, W fragment offsets
+  const float* aseg[NSLOT][2];
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < 4; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int kc = w; kc < nkc; kc += 4) {
-    float4 a[TM][4], bw[4][4];
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-      const float* ap = asrc.ptr(rb * 16 * TM + tm * 16 + r, kc * 64 + g * 16);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        a[tm][q] = ap ? *reinterpret_cast<const float4*>(ap + q * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int tn = 0; tn < 4; ++tn) {
-      const float* wb = Wf + ((size_t)(nb * 4 + tn) * nkc + kc) * FRAG + lane * 4;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bw[tn][q] = *reinterpret_cast<const float4*>(wb + q * 256);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < 4; ++tn) {
-          acc[tm][tn] = mfma16x16x4(a[tm][q].x, bw[tn][q].x, acc[tm][tn]);
-          acc[tm][tn] = mfma16x16x4(a[tm][q].y, bw[tn][q].y, acc[tm][tn]);
-          acc[tm][tn] = mfma16x16x4(a[tm][q].z, bw[tn][q].z, acc[tm][tn]);
-          acc[tm][tn] = mfma16x16x4(a[tm][q].w, bw[tn][q].w, acc[tm][tn]);
-        }
+  for (int j = 0; j < NSLOT; ++j) {
+    const int i = w + 8 * j;
+    aseg[j][0] = aseg[j][1] = nullptr;
+    if (i < NA) asrc.bind(rb * BM + 4 * i + (lane >> 4), aseg[j][0], aseg[j][1]);
   }
+  auto stage = [&](float* dst, int kt) {
+    float* la = dst;
+    float* lw = dst + ATILE;
+    const int k0 = kt * DG_BK;
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm)
+    for (int j = 0; j < NSLOT; ++j) {
+      const int i = w + 8 * j;
+      if (i < NA) {
+        const int row = 4 * i + (lane >> 4), c = (lane & 15) ^ (row & 15);
+        const float* src = k0 < ASrc::kSeg ? aseg[j][0] + k0 : aseg[j][1] + (k0 - ASrc::kSeg);
+        lds_dma16(src + c * 4, la + i * 256);
+      } else if (i < NDMA) {
+        const int tn = (i - NA) >> 2, qq = (i - NA) & 3;
+        lds_dma16(Wf + ((size_t)(nb * 4 + tn) * nkt + kt) * FRAG + qq * 256 + lane * 4, lw + tn * FRAG + qq * 256);
+      }
+    }
+  };
+
+  f32x4 acc[4];
 #pragma unroll
-    for (int tn = 0; tn < 4; ++tn) red.v[w][tm][tn][lane] = acc[tm][tn];
+  for (int tn = 0; tn < 4; ++tn) acc[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow = ws * 16 + r;
+  auto compute = [&](const float* src) {
+    const float* la = src;
+    const float* lw = src + ATILE;
+#pragma unroll
+    for (int qh = 0; qh < QPW; ++qh) {
+      const int q = kq * QPW + qh;
+      const float4 a = *reinterpret_cast<const float4*>(la + arow * DG_BK + (((4 * g + q) ^ (arow & 15)) << 2));
+      float4 b[4];
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) b[tn] = *reinterpret_cast<const float4*>(lw + tn * FRAG + q * 256 + lane * 4);
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) {
+        acc[tn] = mfma16x16x4(a.x, b[tn].x, acc[tn]);
+        acc[tn] = mfma16x16x4(a.y, b[tn].y, acc[tn]);
+        acc[tn] = mfma16x16x4(a.z, b[tn].z, acc[tn]);
+        acc[tn] = mfma16x16x4(a.w, b[tn].w, acc[tn]);
+      }
+    }
+  };
+  stage(buf0, 0);
   __syncthreads();
-  epi.run(red, rb, nb);
+  for (int kt = 0; kt < nkt; kt += 2) {
+    if (kt + 1 < nkt) stage(buf1, kt + 1);
+    compute(buf0);
+    __syncthreads();  // retires this wave's DMA into buf1 and everyone's reads of buf0
+    if (kt + 1 >= nkt) break;
+    if (kt + 2 < nkt) stage(buf0, kt + 2);
+    compute(buf1);
+    __syncthreads();
+  }
+  // k slices 1..KQ-1 hand their partial sums to slice 0 through LDS (free after the last barrier)
+  f32x4* part = reinterpret_cast<f32x4*>(buf0);
+  static_assert((KQ - 1) * WR * 4 * 64 * 16 <= (ATILE + DG_TILE) * 4, "partials fit one stage buffer");
+  if (kq > 0) {
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) part[(((kq - 1) * WR + ws) * 4 + tn) * 64 + lane] = acc[tn];
+  }
+  __syncthreads();
+  if (kq > 0) return;
+#pragma unroll
+  for (int j = 0; j < KQ - 1; ++j)
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) acc[tn] += part[((j * WR + ws) * 4 + tn) * 64 + lane];
+  // lane holds rows rb*BM + ws*16 + 4g + e (e = 0..3), column nb*64 + tn*16 + r
+  epi.run(acc, rb * BM + ws * 16 + 4 * g, nb, r);
 }
 
-// A rows of the decoder LSTM: [embed(tok[r]) | st_old[src[r]][0:1024] = ctx | h]
+// 64-row blocks where that still gives >= 2 blocks per CU, else 32-row blocks
+template <class ASrc, class Epi>
+static void launch_dgemm(int NB, int R, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi, hipStream_t s) {
+  const int NR64 = (R + 63) / 64;
+  if ((int)xcd_grid(NB, NR64) >= 512) {
+    hipLaunchKernelGGL((dgemm_kernel<4, ASrc, Epi>), dim3(xcd_grid(NB, NR64)), dim3(512), 0, s, NB, NR64, nkt, Wf,
+                       asrc, epi);
+  } else {
+    const int NR32 = (R + 31) / 32;
+    hipLaunchKernelGGL((dgemm_kernel<2, ASrc, Epi>), dim3(xcd_grid(NB, NR32)), dim3(512), 0, s, NB, NR32, nkt, Wf,
+                       asrc, epi);
+  }
+}
+
+// A rows of the decoder LSTM: [embed(tok[r]) | st_old[src[r]][0:1024] = ctx | h]; a 64-deep
+// k tile lies in one segment (E = 256 is a multiple of 64).  Rows >= R read row R-1 (unused).
 struct DecLstmA {
+  static constexpr int kSeg = E;  // k < kSeg: embedding row, else state row
   const float* emb;
   const float* st_old;
   const int32_t* tok;
   const int32_t* src;
   int32_t* err;
   int R, V;
-  __device__ __forceinline__ const float* ptr(int row, int k) const {
-    if (row >= R) return nullptr;
-    if (k < E) {
-      int t = tok[row];
-      if ((unsigned)t >= (unsigned)V) {
-        atomicOr(err, CASR_DEV_BAD_TOKEN);
-        t = 0;
-      }
-      return emb + (size_t)t * E + k;
+  __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1) const {
+    row = row < R ? row : R - 1;
+    int t = tok[row];
+    if ((unsigned)t >= (unsigned)V) {
+      atomicOr(err, CASR_DEV_BAD_TOKEN);
+      t = 0;
     }
-    return st_old + (size_t)safe_src(row) * ST + (k - E);
+    seg0 = emb + (size_t)t * E;
+    seg1 = st_old + (size_t)safe_src(row) * ST;
   }
   __device__ __forceinline__ int safe_src(int row) const {
     const int s = src[row];
@@ -131,7 +196,8 @@ struct DecLstmA {
   }
 };
 
-template <int TM>
+// LSTMCell epilogue: the 4 n-tiles of a 64-column block are the 4 gates of 16 hidden units
+// (gate-interleaved packing), so each lane holds all four gates of its (row, unit) cells.
 struct DecLstmEpi {
   const float* bias;  // packed [4HD]
   const float* st_old;
@@ -140,17 +206,18 @@ struct DecLstmEpi {
   const int32_t* newdone;
   int R, l, total;
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
-  __device__ __forceinline__ void run(const RedTile<TM>& red, int rb, int nb) const {
-    for (int idx = threadIdx.x; idx < 16 * TM * 16; idx += 256) {
-      const int rowl = idx >> 4, u = idx & 15;
-      const int row = rb * 16 * TM + rowl;
-      if (row >= R) continue;
-      float gate[4];
+  __device__ __forceinline__ void run(const f32x4 (&acc)[4], int row0, int nb, int u) const {
+    const int U = nb * 16 + u;
+    float bg[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) gate[g] = red.get(rowl, g * 16 + u) + bias[nb * 64 + g * 16 + u];
-      const int U = nb * 16 + u;
+    for (int g = 0; g < 4; ++g) bg[g] = bias[nb * 64 + g * 16 + u];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = row0 + e;
+      if (row >= R) break;
       float h2, c2;
-      lstm_cell(gate[0], gate[1], gate[2], gate[3], st_old[(size_t)rows.safe_src(row) * ST + C + HD + U], h2, c2);
+      lstm_cell(acc[0][e] + bg[0], acc[1][e] + bg[1], acc[2][e] + bg[2], acc[3][e] + bg[3],
+                st_old[(size_t)rows.safe_src(row) * ST + C + HD + U], h2, c2);
       st_new[(size_t)row * ST + C + U] = h2;
       st_new[(size_t)row * ST + C + HD + U] = c2;
     }
@@ -158,25 +225,29 @@ struct DecLstmEpi {
 };
 
 struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h]
+  static constexpr int kSeg = 0;
   const float* st;
   int R;
-  __device__ __forceinline__ const float* ptr(int row, int k) const {
-    return row < R ? st + (size_t)row * ST + k : nullptr;
+  __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1) const {
+    seg0 = seg1 = st + (size_t)(row < R ? row : R - 1) * ST;
   }
 };
 
-template <int TM>
 struct ProjEpi {
   const float* bias;
   float* logits;
   const int32_t* newdone;
   int R, V, l, total;
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
-  __device__ __forceinline__ void run(const RedTile<TM>& red, int rb, int nb) const {
-    for (int idx = threadIdx.x; idx < 16 * TM * 64; idx += 256) {
-      const int rowl = idx >> 6, coll = idx & 63;
-      const int row = rb * 16 * TM + rowl, n = nb * 64 + coll;
-      if (row < R && n < V) logits[(size_t)row * V + n] = red.get(rowl, coll) + bias[n];
+  __device__ __forceinline__ void run(const f32x4 (&acc)[4], int row0, int nb, int u) const {
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const int n = nb * 64 + tn * 16 + u;
+      if (n >= V) continue;
+      const float bn = bias[n];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (row0 + e < R) logits[(size_t)(row0 + e) * V + n] = acc[tn][e] + bn;
     }
   }
 };
@@ -614,12 +685,9 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   float* st_new = d.st[(l + 1) & 1];
   {
     ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
-    constexpr int TM = 1;
     DecLstmA asrc{a.W + a.L.emb, st_old, d.tok[l & 1], d.src[l & 1], d.err, R, a.V};
-    DecLstmEpi<TM> epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, R, l, total};
-    const int NB = HD / 16, NR = (R + 16 * TM - 1) / (16 * TM);
-    hipLaunchKernelGGL((rowgemm_kernel<TM, DecLstmA, DecLstmEpi<TM>>), dim3(xcd_grid(NB, NR)), dim3(256),
-                       0, s, NB, NR, KDEC / 64, a.W + a.L.dec_w, asrc, epi);
+    DecLstmEpi epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, R, l, total};
+    launch_dgemm(HD / 16, R, KDEC / DG_BK, a.W + a.L.dec_w, asrc, epi, s);
   }
   hipError_t e;
   {
@@ -629,12 +697,9 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   if (e != hipSuccess) return e;
   {
     ProfScope ps(a.prof, CASR_K_PROJ, s);
-    constexpr int TM = 2;
     ProjA asrc{st_new, R};
-    ProjEpi<TM> epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total};
-    const int NB = a.L.VP / 64, NR = (R + 16 * TM - 1) / (16 * TM);
-    hipLaunchKernelGGL((rowgemm_kernel<TM, ProjA, ProjEpi<TM>>), dim3(xcd_grid(NB, NR)), dim3(256), 0, s,
-                       NB, NR, KPROJ / 64, a.W + a.L.proj_w, asrc, epi);
+    ProjEpi epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total};
+    launch_dgemm(a.L.VP / 64, R, KPROJ / DG_BK, a.W + a.L.proj_w, asrc, epi, s);
   }
   return hipGetLastError();
 }

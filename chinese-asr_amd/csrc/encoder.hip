@@ -22,19 +22,22 @@ namespace casr {
 // C[M][N] = epilogue(A[M][K] . W[N][K]^T); 256 threads, 128x128 tile, BK = 32, 2x2 waves of
 // 64x64 (4x4 MFMA tiles).  The k order inside a BK tile is permuted identically for A and
 // W (lane group g takes k = 8g + 4*half + e) so each lane's A/W fragment is a contiguous
-// float4 in LDS (ds_read_b128).  Row stride LDK = 36 floats keeps the reads ~conflict-free.
-constexpr int GB_M = 128, GB_N = 128, GB_K = 32, GB_LDK = GB_K + 4;
+// float4 in LDS (ds_read_b128).  K must be a multiple of 4 (a partial last k tile is zero-filled).
+constexpr int GB_M = 128, GB_N = 128, GB_K = 32;
 
-struct StoreBiasEpi {  // C[row][col] = acc + bias[col]
+struct StoreBiasEpi {  // C[row][col] = acc + bias[col]; N % 4 == 0, rows 16 B aligned
+  static constexpr bool kRowTile = true;
   float* C;
   const float* bias;
   int ldc;
-  __device__ __forceinline__ void operator()(int row, int col, float v) const {
-    C[(size_t)row * ldc + col] = v + bias[col];
+  __device__ __forceinline__ float4 bias4(int col) const { return *reinterpret_cast<const float4*>(bias + col); }
+  __device__ __forceinline__ void store4(int row, int col, float4 v) const {
+    *reinterpret_cast<float4*>(C + (size_t)row * ldc + col) = v;
   }
 };
 
 struct KeysEpi {  // keysT[b][a][t] = acc + b_attn[a], row = b*Tp + t, row stride Tq
+  static constexpr bool kRowTile = false;
   float* keysT;
   const float* bias;
   int Tp, Tq;
@@ -69,11 +72,22 @@ inline TileOrder tile_order(int NB, int NM, int K) {
 }
 
 template <class Epi>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ Amat, int lda,
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ Amat, int lda,
                                                       const float* __restrict__ Wmat, int ldw,
                                                       int M, int N, int K, TileOrder order, Epi epi) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * (GB_M + GB_N) * GB_LDK];
-  constexpr int STAGE = (GB_M + GB_N) * GB_LDK;  // one buffer: A tile then W tile
+  // Operand tiles are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4): no VGPR round
+  // trip, so the next tile's loads stay in flight under all 128 MFMAs of the current one
+  // (tools/probes/gemm_ablate.hip).  The two stage buffers are two distinct __shared__ arrays and
+  // the k loop is unrolled by 2, so hipcc proves the in-flight DMA does not alias the ds_reads of
+  // the other buffer (with one array and a runtime index it drained the DMA before every tile).
+  // Rows are 128 B, lane-linear; the 16-B chunk c of row r sits at c ^ ((r >> 1) & 7) (XOR on the
+  // per-lane SOURCE address, read back with the same XOR) so a ds_read_b128 over 16 rows hits 16
+  // distinct bank slots.
+  constexpr int TILE = GB_M * GB_K;  // floats per operand tile (16 KB)
+  constexpr int LDC = GB_N + 4;      // epilogue row stride (32-row quarters)
+  static_assert(32 * LDC <= 2 * TILE, "epilogue quarter fits one stage buffer");
+  __shared__ __attribute__((aligned(16))) float buf0[2 * TILE];  // [A tile | W tile]
+  __shared__ __attribute__((aligned(16))) float buf1[2 * TILE];
 
   int nt, mt;
   if (!order.tile(blockIdx.x, nt, mt)) return;
@@ -88,48 +102,51 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ 
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float4 ra[4], rw[4];
-  auto gload = [&](int k0) {
+  // wave w stages rows [32w, 32w + 32) of the A and W tiles: 4 + 4 DMA instructions of 8 rows;
+  // rows past M / N are clamped (their results are never stored)
+  auto stage = [&](float* dst, int k0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * 256;
-      const int row = idx >> 3, c4 = idx & 7;
-      const int kk = k0 + c4 * 4;
-      const int ar = m0 + row, wr = n0 + row;
-      ra[i] = (ar < M && kk < K) ? *reinterpret_cast<const float4*>(Amat + (size_t)ar * lda + kk)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-      rw[i] = (wr < N && kk < K) ? *reinterpret_cast<const float4*>(Wmat + (size_t)wr * ldw + kk)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int row = wave * 32 + i * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+      const int ar = min(m0 + row, M - 1), wr = min(n0 + row, N - 1);
+      float* la = dst + (wave * 32 + i * 8) * GB_K;
+      __builtin_amdgcn_global_load_lds(Amat + (size_t)ar * lda + k0 + c * 4,
+                                       (__attribute__((address_space(3))) void*)la, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Wmat + (size_t)wr * ldw + k0 + c * 4,
+                                       (__attribute__((address_space(3))) void*)(la + TILE), 16, 0, 0);
     }
   };
-  auto swrite = [&](int buf) {
+  // partial last k tile (K = 720 = 22.5 tiles): register loads, zeros past K, same swizzle
+  auto stage_partial = [&](float* dst, int k0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * 256;
-      const int row = idx >> 3, c4 = idx & 7;
-      *reinterpret_cast<float4*>(smem + buf * STAGE + row * GB_LDK + c4 * 4) = ra[i];
-      *reinterpret_cast<float4*>(smem + buf * STAGE + (GB_M + row) * GB_LDK + c4 * 4) = rw[i];
+      const int idx = tid + i * 256, row = idx >> 3, c = idx & 7, kk = k0 + c * 4;
+      const int ar = min(m0 + row, M - 1), wr = min(n0 + row, N - 1);
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 va = kk < K ? *reinterpret_cast<const float4*>(Amat + (size_t)ar * lda + kk) : z;
+      const float4 vw = kk < K ? *reinterpret_cast<const float4*>(Wmat + (size_t)wr * ldw + kk) : z;
+      float* la = dst + row * GB_K + ((c ^ ((row >> 1) & 7)) << 2);
+      *reinterpret_cast<float4*>(la) = va;
+      *reinterpret_cast<float4*>(la + TILE) = vw;
     }
   };
-
-  const int nk = (K + GB_K - 1) / GB_K;
-  gload(0);
-  swrite(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * GB_K);
-    const float* as = smem + cur * STAGE;
-    const float* ws = as + GB_M * GB_LDK;
+  auto compute = [&](const float* src) {
+    const float* as = src;
+    const float* ws = src + TILE;
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
+      const int c = g * 2 + half;  // logical chunk of k = 8g + 4 half (same k order as the MFMA)
       float4 a[4], w[4];
 #pragma unroll
-      for (int tm = 0; tm < 4; ++tm)
-        a[tm] = *reinterpret_cast<const float4*>(as + (wm * 64 + tm * 16 + r) * GB_LDK + g * 8 + half * 4);
+      for (int tm = 0; tm < 4; ++tm) {
+        const int row = wm * 64 + tm * 16 + r;
+        a[tm] = *reinterpret_cast<const float4*>(as + row * GB_K + ((c ^ ((row >> 1) & 7)) << 2));
+      }
 #pragma unroll
-      for (int tn = 0; tn < 4; ++tn)
-        w[tn] = *reinterpret_cast<const float4*>(ws + (wn * 64 + tn * 16 + r) * GB_LDK + g * 8 + half * 4);
+      for (int tn = 0; tn < 4; ++tn) {
+        const int row = wn * 64 + tn * 16 + r;
+        w[tn] = *reinterpret_cast<const float4*>(ws + row * GB_K + ((c ^ ((row >> 1) & 7)) << 2));
+      }
 #pragma unroll
       for (int tm = 0; tm < 4; ++tm)
 #pragma unroll
@@ -140,26 +157,78 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const float* __restrict__ 
           acc[tm][tn] = mfma16x16x4(a[tm].w, w[tn].w, acc[tm][tn]);
         }
     }
-    if (kt + 1 < nk) swrite(cur ^ 1);
+  };
+
+  const int nk = K / GB_K;  // full tiles, staged by DMA
+  if (nk > 0) {
+    stage(buf0, 0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; kt += 2) {
+    if (kt + 1 < nk) stage(buf1, (kt + 1) * GB_K);
+    compute(buf0);
+    __syncthreads();  // retires this wave's DMA into buf1 and everyone's reads of buf0
+    if (kt + 1 >= nk) break;
+    if (kt + 2 < nk) stage(buf0, (kt + 2) * GB_K);
+    compute(buf1);
+    __syncthreads();
+  }
+  if (nk * GB_K < K) {  // both buffers are free here
+    stage_partial(buf0, nk * GB_K);
+    __syncthreads();
+    compute(buf0);
     __syncthreads();
   }
 
+  if constexpr (Epi::kRowTile) {
+    // stage the tile through LDS in four 32-row quarters and store whole rows: 16 B per lane
+    const int c4 = tid & 31, r0 = tid >> 5;  // 32 float4 per row, 8 rows per pass
+    const int col = n0 + c4 * 4;
+    const float4 bias4 = col < N ? epi.bias4(col) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int tm = 0; tm < 4; ++tm)
+    for (int p = 0; p < 4; ++p) {
+      // quarter p = rows [32p, 32p + 32): tiles tm in {2(p&1), 2(p&1)+1} of the waves with wm = p >> 1
+      if (wm == (p >> 1)) {
 #pragma unroll
-    for (int tn = 0; tn < 4; ++tn) {
-      const int col = n0 + wn * 64 + tn * 16 + r;
+        for (int th = 0; th < 2; ++th) {
+          const int tm = 2 * (p & 1) + th;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wm * 64 + tm * 16 + g * 4 + e;
-        if (row < M && col < N) epi(row, col, acc[tm][tn][e]);
+          for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              buf0[(th * 16 + g * 4 + e) * LDC + wn * 64 + tn * 16 + r] = acc[tm][tn][e];
+        }
       }
+      __syncthreads();
+      if (col < N) {
+#pragma unroll
+        for (int row = r0; row < 32; row += 8) {
+          if (m0 + p * 32 + row >= M) break;
+          const float4 v = *reinterpret_cast<const float4*>(buf0 + row * LDC + c4 * 4);
+          epi.store4(m0 + p * 32 + row, col, make_float4(v.x + bias4.x, v.y + bias4.y, v.z + bias4.z, v.w + bias4.w));
+        }
+      }
+      __syncthreads();
     }
+  } else {
+#pragma unroll
+    for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) {
+        const int col = n0 + wn * 64 + tn * 16 + r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = m0 + wm * 64 + tm * 16 + g * 4 + e;
+          if (row < M && col < N) epi(row, col, acc[tm][tn][e]);
+        }
+      }
+  }
 }
 
 hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, const float* bias,
                              float* Gin, hipStream_t s) {
   const int N = 8 * H;
+  if (Din % 4 != 0 || M <= 0) return hipErrorInvalidValue;  // 16-B rows chunks (K tail: gemm_nt_kernel)
   StoreBiasEpi epi{Gin, bias, N};
   const TileOrder order = tile_order(N / GB_N, (M + GB_M - 1) / GB_M, Din);
   hipLaunchKernelGGL(gemm_nt_kernel<StoreBiasEpi>, dim3(order.blocks()), dim3(256), 0, s, X, Din, W,
@@ -170,6 +239,7 @@ hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, con
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s) {
   const int M = B * Tp;
+  if (M <= 0) return hipErrorInvalidValue;
   KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3};
   const TileOrder order = tile_order(A / GB_N, (M + GB_M - 1) / GB_M, C);
   hipLaunchKernelGGL(gemm_nt_kernel<KeysEpi>, dim3(order.blocks()), dim3(256), 0, s, enc, C, wencT,
