@@ -107,22 +107,37 @@ def to_numpy_sd(sd):
     return out
 
 
-def load_checkpoint(path):
-    """Read a reference ``.ckpt`` (model.py:357-370) without executing pickled code.
+class TrainVar(object):
+    """Behaviour-free stand-in for the reference's training record ``util.TrainVar``
+    (util.py:2356-2363), which ``Model.save`` stores as ``args`` (model.py:347-355).  Registered
+    with torch's weights-only unpickler under the reference's module/name, so the safe loader
+    rebuilds it by plain attribute assignment: nothing from the file is executed."""
 
-    ``torch.load(weights_only=True)`` refuses arbitrary classes, which the reference's
-    ``args`` entry (a pickled ``TrainVar``, util.py:2356) may be; such a file is refused
-    with a RuntimeError naming the remedy (nothing from it is executed).
+    def __init__(self, step=None, loss=None, best_wer=None, lr=None, duration=None, num_no_imprv=None):
+        self.step, self.loss, self.best_wer = step, loss, best_wer
+        self.lr, self.duration, self.num_no_imprv = lr, duration, num_no_imprv
+
+    def __repr__(self):
+        return f"TrainVar({self.__dict__})"
+
+
+TrainVar.__module__ = "util"
+
+
+def load_checkpoint(path):
+    """Read a reference ``.ckpt`` (model.py:357-370) without executing pickled code:
+    ``torch.load(weights_only=True)`` with the reference's ``util.TrainVar`` record allow-listed
+    as the plain stand-in above.  Any other non-tensor object is refused with a RuntimeError.
     Returns ``(enc_sd, dec_sd, args)``."""
     import torch
     try:
-        ck = torch.load(path, map_location="cpu", weights_only=True)
-        args = ck.get("args")
-    except Exception as e:  # an 'args' object the safe loader will not build
+        with torch.serialization.safe_globals([TrainVar]):
+            ck = torch.load(path, map_location="cpu", weights_only=True)
+    except Exception as e:  # an object the safe loader will not build
         raise RuntimeError(
             f"{path}: refused by the weights_only loader ({e}). Re-save the checkpoint "
             f"with only tensors (encoder_state_dict/decoder_state_dict)") from None
-    return to_numpy_sd(ck["encoder_state_dict"]), to_numpy_sd(ck["decoder_state_dict"]), args
+    return to_numpy_sd(ck["encoder_state_dict"]), to_numpy_sd(ck["decoder_state_dict"]), ck.get("args")
 
 
 def save_checkpoint(path, enc_sd, dec_sd, args=None):

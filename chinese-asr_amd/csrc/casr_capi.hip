@@ -448,7 +448,7 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
       // diagnostics only: CASR_REC_TRACE=<file> dumps per-wave phase timestamps of layer 0
       const char* trace_path = l == 0 ? std::getenv("CASR_REC_TRACE") : nullptr;
       DevBuf tbuf;
-      const size_t tbytes = (size_t)rec_layer_grid_blocks(B) * 8 * Tp * 5 * sizeof(uint32_t);
+      const size_t tbytes = (size_t)rec_layer_grid_blocks(B) * rec_layer_waves() * Tp * 5 * sizeof(uint32_t);
       if (trace_path) {
         HIP_OK(h, tbuf.ensure(tbytes));
         HIP_OK(h, hipMemsetAsync(tbuf.p, 0, tbytes, s));
@@ -466,7 +466,7 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
         HIP_OK(h, hipStreamSynchronize(s));
         tbuf.release();
         if (FILE* f = std::fopen(trace_path, "wb")) {
-          const int32_t hdr[4] = {rec_layer_grid_blocks(B), 8, Tp, 5};
+          const int32_t hdr[4] = {rec_layer_grid_blocks(B), rec_layer_waves(), Tp, 5};
           std::fwrite(hdr, sizeof hdr, 1, f);
           std::fwrite(hostv.data(), 4, hostv.size(), f);
           std::fclose(f);

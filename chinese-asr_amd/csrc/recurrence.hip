@@ -31,6 +31,8 @@
 // (0 for inactive and padding rows) so no wait depends on lengths.  Spins are bounded (~2 s of
 // s_memrealtime and a pass count); a timeout sets CASR_DEV_REC_TIMEOUT and the workgroup leaves
 // the loop.
+#include <stdlib.h>
+
 #include "casr_common.h"
 #include "casr_internal.h"
 
@@ -38,7 +40,6 @@ namespace casr {
 
 namespace {
 
-constexpr int RG = 32;                 // batch rows per workgroup
 constexpr int NKC = H / 64;            // 4 k-chunks of 64 hidden units
 constexpr uint64_t SPIN_TICKS = 200000000ull;  // s_memrealtime runs at 100 MHz: 2 s
 
@@ -59,12 +60,15 @@ CASR_DEV float decode_granule(uint32_t x) {
   return (x & 0x7FFFFFFFu) == NONFINITE ? __uint_as_float(0x7FC00000u) : __uint_as_float(x);
 }
 
-__global__ __launch_bounds__(512, 2) void rec_layer_kernel(
+// RG batch rows per workgroup (32: 8 waves, one workgroup per CU; 16: 4 waves, two per CU)
+template <int RG>
+__global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
     int32_t* __restrict__ err, uint32_t* __restrict__ trace) {
-  __shared__ f32x4 red[2][8][4][64];  // double-buffered k-chunk partials (64 KB)
+  constexpr int NW = RG / 4;           // waves: 4 k-chunks x RG/16 row halves
+  __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
   const int ub = blockIdx.x, rg = blockIdx.y, d = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(512, 2) void rec_layer_kernel(
     }
   };
   load_operands(0, gin_v, x_res);
-  uint32_t* tr = trace ? trace + ((size_t)((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 8 + w) * Tp * 5 : nullptr;
+  uint32_t* tr = trace ? trace + ((size_t)((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * NW + w) * Tp * 5 : nullptr;
   for (int s = 0; s < tmax; ++s) {
     const bool act = s < len;
     uint32_t npass = 0;
@@ -213,15 +217,27 @@ __global__ __launch_bounds__(512, 2) void rec_layer_kernel(
 
 }  // namespace
 
+static int rec_rg() {  // CASR_REC_RG=16 selects 16-row workgroups (diagnostics / tuning)
+  static const int rg = [] {
+    const char* e = std::getenv("CASR_REC_RG");
+    return (e && std::atoi(e) == 16) ? 16 : 32;
+  }();
+  return rg;
+}
+
 size_t rec_layer_granule_bytes(int B) {
-  const int Bp = (B + RG - 1) / RG * RG;
+  const int Bp = (B + 31) / 32 * 32;
   return (size_t)3 * 2 * Bp * H * sizeof(uint32_t);
 }
 
-int rec_layer_grid_blocks(int B) { return (H / 16) * ((B + RG - 1) / RG) * 2; }
+int rec_layer_waves() { return rec_rg() / 4; }
+
+int rec_layer_grid_blocks(int B) { return (H / 16) * ((B + rec_rg() - 1) / rec_rg()) * 2; }
 
 hipError_t rec_layer_occupancy(int* blocks_per_cu) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rec_layer_kernel, 512, 0);
+  return rec_rg() == 16
+             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rec_layer_kernel<16>, 256, 0)
+             : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rec_layer_kernel<32>, 512, 0);
 }
 
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
@@ -235,9 +251,14 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int32_t* err, uint32_t* trace, hipStream_t s) {
-  const int Bp = (B + RG - 1) / RG * RG;
-  dim3 grid(H / 16, Bp / RG, 2);
-  hipLaunchKernelGGL(rec_layer_kernel, grid, dim3(512), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens,
+  const int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for either RG
+  const int RG = rec_rg();
+  dim3 grid(H / 16, (B + RG - 1) / RG, 2);
+  if (RG == 16)
+    hipLaunchKernelGGL(rec_layer_kernel<16>, grid, dim3(256), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens,
+                       B, Bp, Tp, residual, err, trace);
+  else
+    hipLaunchKernelGGL(rec_layer_kernel<32>, grid, dim3(512), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens,
                      B, Bp, Tp, residual, err, trace);
   return hipGetLastError();
 }

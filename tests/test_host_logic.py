@@ -66,3 +66,48 @@ def test_wer():
     assert edit_distance("", "abc") == 3
     assert edit_distance("kitten", "sitting") == 3
     assert get_wer("ab", "abcd") == 0.5
+
+
+def test_checkpoint_roundtrip_with_reference_trainvar(tmp_path):
+    """A checkpoint in the reference's own format (Model.save, model.py:347-355: state dicts,
+    optimizer state, and ``args`` = a pickled util.TrainVar, util.py:2356) loads through the
+    weights-only path: tensors bit-exact, the TrainVar fields readable, nothing executed."""
+    import sys
+    import types
+
+    import numpy as np
+    import torch
+
+    from casr.config import CasrConfig
+    from casr.weights import load_checkpoint, synthetic_state_dicts
+
+    cfg = CasrConfig()
+    enc_sd, dec_sd = synthetic_state_dicts(cfg, peaked=True)
+    fake = types.ModuleType("util")  # what the reference pickles: util.TrainVar
+
+    class TrainVar(object):
+        def __init__(self, step, loss, best_wer, lr, duration, num_no_imprv):
+            self.step, self.loss, self.best_wer = step, loss, best_wer
+            self.lr, self.duration, self.num_no_imprv = lr, duration, num_no_imprv
+
+    TrainVar.__module__, TrainVar.__qualname__ = "util", "TrainVar"
+    fake.TrainVar = TrainVar
+    saved = sys.modules.get("util")
+    sys.modules["util"] = fake
+    try:
+        path = str(tmp_path / "ref.ckpt")
+        torch.save({"encoder_state_dict": {k: torch.from_numpy(v) for k, v in enc_sd.items()},
+                    "decoder_state_dict": {k: torch.from_numpy(v) for k, v in dec_sd.items()},
+                    "optimizer_state_dict": {"state": {}, "param_groups": [{"lr": 1e-3, "params": [0, 1]}]},
+                    "args": TrainVar(12000, 0.731, 0.06328, 1e-4, 3.5, 2)}, path)
+    finally:
+        if saved is None:
+            del sys.modules["util"]
+        else:
+            sys.modules["util"] = saved
+    e2, d2, args = load_checkpoint(path)
+    for a, b in ((enc_sd, e2), (dec_sd, d2)):
+        assert list(a) == list(b)
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k])
+    assert args.step == 12000 and abs(args.best_wer - 0.06328) < 1e-12 and args.num_no_imprv == 2

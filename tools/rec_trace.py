@@ -40,7 +40,7 @@ def main(B=256, T=800, path="/tmp/rec_trace.bin"):
     period = t[:, :, 2:, 0] - t[:, :, 1:-1, 0]
     passes = tr[:, :, 1:, 4]
     # grid order: blockIdx.x = 16 unit blocks, then row groups, then directions
-    ngrp = nwg // 16
+    ngrp = nwg // 16  # (row group, direction) groups of 16 producer workgroups
     st = t[:, :, :, 3].max(axis=1).reshape(ngrp, 16, Tp)          # WG's last store per step
     done = t[:, :, :, 1].reshape(ngrp, 16, nw, Tp)
     lat = done[:, :, :, 1:] - st.max(axis=1)[:, None, None, :-1]
