@@ -61,10 +61,24 @@ LAUNCH_UNIT = {
     "rec_step": "rec_layer_kernel: one encoder layer, all Tp steps, both directions, B rows "
                 "(per-step launches rec_step_kernel when the persistent grid does not fit)",
     "input_proj": "gemm_nt_kernel<StoreBiasEpi>: one layer's input projection, B*Tp rows",
-    "proj": "rowgemm_kernel<2,ProjA>: one decode step's vocabulary projection",
-    "dec_lstm": "rowgemm_kernel<1,DecLstmA>: one decode step's LSTMCell",
+    "proj": "dgemm_kernel<*,ProjA>: one decode step's vocabulary projection",
+    "dec_lstm": "dgemm_kernel<*,DecLstmA>: one decode step's LSTMCell",
     "attention": "attention_kernel: one decode step",
 }
+
+
+def kernel_bytes(cls, B, Tp, R, V):
+    """Algorithmic HBM bytes of ONE launch of a kernel class (compulsory reads + writes), to set
+    beside the PMC-measured traffic; None where not tabulated."""
+    H, C, D, A = 256, 512, 720, 128
+    if cls == "input_proj":  # average layer: X read, W_ih read, Gin written
+        k = (D + 3 * C) / 4.0
+        return 4.0 * (B * Tp * k + 8 * H * k + B * Tp * 8 * H)
+    if cls == "rec_step":    # Gin read, layer output written (h exchange is on-chip traffic)
+        return 4.0 * (B * Tp * 8 * H + B * Tp * C)
+    if cls == "attention":
+        return 4.0 * B * Tp * (A + C)
+    return None
 
 
 def cpu_baseline(n_utt, T):
@@ -189,11 +203,14 @@ def main():
         achieved, peak, unit = per_launch_work / avg_launch_s / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"
     else:
         achieved, peak, unit = per_launch_work / avg_launch_s / 1e9, PEAK_HBM_GBS, "GB/s"
+    # HBM/fabric bytes per launch of the dominant kernel from the committed PMC passes
+    # (tools/probes/pmc_passes.sh -> tools/pmc_summary.py --json: 2 x FETCH_SIZE + WRITE_SIZE)
     traffic = None
     pmc_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_file):
         try:
-            traffic = json.load(open(pmc_file)).get(dominant)
+            rec = json.load(open(pmc_file)).get(dominant)
+            traffic = float(rec["hbm_bytes"]) if rec else None
         except Exception:
             traffic = None
 
@@ -233,6 +250,8 @@ def main():
             "beam": beam,
             "roofline": {"kernel": dominant, "bound": bound, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": achieved / peak, "traffic": traffic,
+                         "traffic_unit": "bytes per launch (PMC 2 x FETCH_SIZE + WRITE_SIZE)",
+                         "algorithmic_bytes": kernel_bytes(dominant, B, Tp, B, cfg.vocab),
                          "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s,
                          "launch": LAUNCH_UNIT.get(dominant, "one kernel launch")},
             "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},

@@ -16,20 +16,22 @@ import os
 import sys
 from collections import defaultdict
 
-CLASS_OF = {  # bench.py kernel classes -> kernel-name prefixes
-    "input_proj": "gemm_nt_kernel<casr::StoreBiasEpi>",
-    "keys": "gemm_nt_kernel<casr::KeysEpi>",
+CLASS_OF = {  # bench.py kernel classes -> kernel-name prefixes (after short())
+    "input_proj": "gemm_nt_kernel<StoreBiasEpi>",
+    "keys": "gemm_nt_kernel<KeysEpi>",
     "rec_step": "rec_layer_kernel",
-    "dec_lstm": "rowgemm_kernel<1",
-    "proj": "rowgemm_kernel<2",
-    "attention": "attention_kernel",
+    "dec_lstm": "dgemm_kernel<2, DecLstmA",
+    "proj": "dgemm_kernel<2, ProjA",
+    "attention": "attention_kernel<1>",
     "select": "greedy_select_kernel",
+    "features": "cmvn_kernel",
 }
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     n = name[:name.index("(")] if "(" in name else name
-    return n.replace("void ", "").replace("casr::", "").replace("(anonymous namespace)::", "")
+    return n.replace("void ", "").replace("casr::", "")
 
 
 def load(d):
