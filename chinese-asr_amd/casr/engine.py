@@ -168,6 +168,15 @@ class Engine:
         """Persistent per-layer recurrence (default on where its grid fits); off = per-step."""
         _lib.check(self.lib.casr_set_persistent(self.handle, int(bool(enable))), self.handle)
 
+    def set_precision(self, precision):
+        """'s16x3' (default: split-f16 MFMA, f32 accumulate) or 'f32' (exact-f32 MFMA)."""
+        _lib.check(self.lib.casr_set_precision(self.handle, _lib.PRECISIONS[precision]), self.handle)
+
+    def precision(self):
+        """Effective arithmetic of the MFMA contractions ('s16x3' or 'f32')."""
+        p = int(self.lib.casr_get_precision(self.handle))
+        return {v: k for k, v in _lib.PRECISIONS.items()}[p]
+
     def recurrence_mode(self, B):
         """1 if casr_encode would run the persistent recurrence for batch B, else 0."""
         return int(self.lib.casr_recurrence_mode(self.handle, int(B)))

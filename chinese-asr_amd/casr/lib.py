@@ -21,8 +21,11 @@ EXPORTS = [
     "casr_gather_utterances", "casr_encode", "casr_encoder_results", "casr_greedy", "casr_beam",
     "casr_beam_records", "casr_profile_enable", "casr_profile_read", "casr_set_graphs",
     "casr_device_flags", "casr_set_persistent", "casr_recurrence_mode", "casr_log_mel",
-    "casr_log_mel_frames", "casr_mel_filterbank",
+    "casr_log_mel_frames", "casr_mel_filterbank", "casr_set_precision", "casr_get_precision",
 ]
+
+# arithmetic of the MFMA contractions (casr_set_precision)
+PRECISIONS = {"f32": 0, "s16x3": 1}
 
 # kernel classes of casr_profile_enable / casr_profile_read (include/casr.h)
 KERNEL_CLASSES = ["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"]
@@ -90,6 +93,8 @@ def load(path=None):
         "casr_device_flags": (i32, [vp, ctypes.POINTER(ctypes.c_int32), vp]),
         "casr_set_persistent": (i32, [vp, i32]),
         "casr_recurrence_mode": (i32, [vp, i32]),
+        "casr_set_precision": (i32, [vp, i32]),
+        "casr_get_precision": (i32, [vp]),
         "casr_log_mel": (i32, [vp, vp, vp, i32, i32, i32, f32, vp, vp, vp]),
         "casr_log_mel_frames": (i32, [i32]),
         "casr_mel_filterbank": (i32, [i32, f32, f32, i32, vp]),

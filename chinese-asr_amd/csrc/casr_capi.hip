@@ -2,6 +2,7 @@
 // per-handle device workspaces, and the encode / decode drivers.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -42,6 +43,12 @@ Layout make_layout(const casr_config& cfg) {
   L.b_attn = take((size_t)A);
   L.w_hidden = take((size_t)HD * A);
   L.v = take((size_t)A);
+  L.info = take(64);
+  for (int l = 0; l < cfg.enc_layers; ++l) {
+    const int din = l == 0 ? D : C;
+    L.enc_wih16[l] = take((size_t)8 * H * s16_kpad(din));
+    L.enc_whh16[l] = take((size_t)2 * 4 * H * H);
+  }
   L.total = off;
   return L;
 }
@@ -60,6 +67,51 @@ static void pack_frag(float* dst, int NT, int NKC, Fn f) {
             const int n = nt * 16 + (lane & 15);
             const int k = kc * 64 + 16 * (lane >> 4) + 4 * q + e;
             blk[(q * 64 + lane) * 4 + e] = f(n, k);
+          }
+    }
+}
+
+// ---- s16x3 images (casr_common.h split16), host side: hi = f16_rn(x), lo = f16_rn((x - hi) 2^11)
+static void split16_host(float x, uint16_t& hi, uint16_t& lo) {
+  const _Float16 h = (_Float16)x;
+  const float r = (x - (float)h) * 2048.0f;
+  const _Float16 l = (r == r && std::fabs(r) < 65504.f) ? (_Float16)r : (_Float16)0.f;
+  std::memcpy(&hi, &h, 2);
+  std::memcpy(&lo, &l, 2);
+}
+
+// [N][K] (accessor f(n, k)) as s16 row images [N][Kp/32][32 hi | 32 lo], zeros past K
+template <class Fn>
+static void pack_rows16(float* dst, int N, int K, Fn f) {
+  const int Kp = s16_kpad(K);
+  uint16_t* o = reinterpret_cast<uint16_t*>(dst);
+  for (int n = 0; n < N; ++n)
+    for (int k = 0; k < Kp; ++k) {
+      uint16_t hi = 0, lo = 0;
+      if (k < K) split16_host(f(n, k), hi, lo);
+      uint16_t* t = o + (size_t)n * Kp * 2 + (k / 32) * 64 + (k % 32);
+      t[0] = hi;
+      t[32] = lo;
+    }
+}
+
+// [N][K] in s16 fragment-major order: 16-row x 64-k blocks of FRAG floats, block (nt, kc) =
+// [j = 0..1][hl = hi, lo][lane][8 halves] with lane row = lane & 15 and
+// k = kc*64 + 16*(lane >> 4) + 8j + e: lane l's v_mfma_f32_16x16x32_f16 B operand for k-step j
+// is one 16-B load, and its 16 k (both steps) are the 16 consecutive k of its f32 fragment row.
+template <class Fn>
+static void pack_frag16(float* dst, int NT, int NKC, Fn f) {
+  uint16_t* o = reinterpret_cast<uint16_t*>(dst);
+  for (int nt = 0; nt < NT; ++nt)
+    for (int kc = 0; kc < NKC; ++kc) {
+      uint16_t* blk = o + ((size_t)nt * NKC + kc) * FRAG * 2;
+      for (int j = 0; j < 2; ++j)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < 8; ++e) {
+            uint16_t hi, lo;
+            split16_host(f(nt * 16 + (lane & 15), kc * 64 + 16 * (lane >> 4) + 8 * j + e), hi, lo);
+            blk[((j * 2 + 0) * 64 + lane) * 8 + e] = hi;
+            blk[((j * 2 + 1) * 64 + lane) * 8 + e] = lo;
           }
     }
 }
@@ -108,6 +160,10 @@ struct casr_handle {
   DevBuf fe_const; // FrontendConst (filterbank, window, twiddles), built on first casr_log_mel
   DevBuf fflag;    // front-end device guard bits (CASR_DEV_BAD_AUDIO)
   bool use_persistent = true;
+  int precision = CASR_PREC_S16X3;  // requested (casr_set_precision)
+  bool s16_valid = false;           // the bound blob's s16 images are usable (Layout::info)
+  DevBuf x16;                       // s16 row image of the current layer input [B*Tp][Kp]
+  bool s16() const { return precision == CASR_PREC_S16X3 && s16_valid; }
   int rec_capacity = 0;  // workgroups of rec_layer_kernel resident at once (CUs x blocks/CU)
   int B = 0, Tp = 0;
   bool encoded = false;
@@ -229,7 +285,22 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
   if (rc) return rc;
   if (!w || !out) return fail(nullptr, CASR_ERR_ARG, "weights/out is NULL");
   const Layout L = make_layout(*cfg);
+  // the s16x3 images need every MFMA weight inside the f16 range with room to spare; blob word
+  // L.info records whether they are usable (casr_bind_weights reads it)
+  auto in_range = [](const float* p, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+      if (!(std::fabs(p[i]) < 16384.f)) return false;
+    return true;
+  };
+  bool s16_ok = true;
+  for (int l = 0; l < cfg->enc_layers; ++l)
+    for (int d = 0; d < 2; ++d)
+      if (w->enc_w_ih[l][d] && w->enc_w_hh[l][d] &&
+          (!in_range(w->enc_w_ih[l][d], (size_t)4 * H * (l == 0 ? D : C)) ||
+           !in_range(w->enc_w_hh[l][d], (size_t)4 * H * H)))
+        s16_ok = false;
   std::memset(out, 0, L.total * sizeof(float));
+  out[L.info] = s16_ok ? 1.f : 0.f;
   const int V = cfg->vocab;
   for (int l = 0; l < cfg->enc_layers; ++l) {
     const int din = l == 0 ? D : C;
@@ -250,11 +321,15 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
     // jb*16 .. jb*16+15
     for (int d = 0; d < 2; ++d) {
       const float* Whh = w->enc_w_hh[l][d];
-      pack_frag(out + L.enc_whh[l] + (size_t)d * 4 * H * H, 4 * H / 16, H / 64, [&](int n, int k) {
+      auto whh = [&](int n, int k) {
         const int jb = n / 64, g = (n / 16) % 4, u = jb * 16 + (n % 16);
         return Whh[(size_t)(g * H + u) * H + k];
-      });
+      };
+      pack_frag(out + L.enc_whh[l] + (size_t)d * 4 * H * H, 4 * H / 16, H / 64, whh);
+      pack_frag16(out + L.enc_whh16[l] + (size_t)d * 4 * H * H, 4 * H / 16, H / 64, whh);
     }
+    const float* wih = out + L.enc_wih[l];
+    pack_rows16(out + L.enc_wih16[l], 8 * H, din, [&](int n, int k) { return wih[(size_t)n * din + k]; });
   }
   if (!w->embedding || !w->dec_w_ih || !w->dec_w_hh || !w->dec_b_ih || !w->dec_b_hh || !w->proj_w ||
       !w->proj_b || !w->attn_w_enc || !w->attn_b || !w->attn_w_hidden || !w->attn_v)
@@ -311,8 +386,26 @@ int casr_create(const casr_config* cfg, int device, casr_handle** out) {
 
 int casr_bind_weights(casr_handle* h, const float* packed_device) {
   if (!h || !packed_device) return fail(h, CASR_ERR_ARG, "handle/weights NULL");
+  HIP_OK(h, hipSetDevice(h->device));
+  float info = 0.f;
+  HIP_OK(h, hipMemcpy(&info, packed_device + h->L.info, sizeof(float), hipMemcpyDeviceToHost));
+  h->s16_valid = info == 1.f;
   h->W = packed_device;
+  h->graphs.clear();  // captured graphs bake in the precision and weight pointers
   return CASR_OK;
+}
+
+int casr_set_precision(casr_handle* h, int precision) {
+  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
+  if (precision != CASR_PREC_F32 && precision != CASR_PREC_S16X3)
+    return fail(h, CASR_ERR_ARG, "unknown precision %d", precision);
+  h->precision = precision;
+  return CASR_OK;
+}
+
+int casr_get_precision(const casr_handle* h) {
+  if (!h) return -1;
+  return h->s16() ? CASR_PREC_S16X3 : CASR_PREC_F32;
 }
 
 void casr_destroy(casr_handle* h) {
@@ -325,7 +418,7 @@ void casr_destroy(casr_handle* h) {
     if (h->ev_out[i]) (void)hipEventDestroy(h->ev_out[i]);
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
-  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->hx, &h->eflag, &h->fe_const, &h->fflag,
+  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->hx, &h->x16, &h->eflag, &h->fe_const, &h->fflag,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout})
     b->release();
   delete h;
@@ -425,6 +518,8 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   HIP_OK(h, h->eflag.ensure(16));
   HIP_OK(h, hipMemsetAsync(h->eflag.p, 0, 16, s));
   const bool persistent = casr_recurrence_mode(h, B) == 1;
+  const bool s16 = h->s16();
+  if (s16) HIP_OK(h, h->x16.ensure(rows * s16_kpad(D) * sizeof(float)));
   if (persistent) HIP_OK(h, h->hx.ensure(rec_layer_granule_bytes(B)));
   const int32_t* dl = h->lens.as<int32_t>();
   float* outs[2] = {h->out0.as<float>(), h->out1.as<float>()};
@@ -435,8 +530,15 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
     float* out = outs[l & 1];
     {
     ProfScope ps(&h->prof, CASR_K_INPUT_PROJ, s);
-    HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
-                                h->gin.as<float>(), s));
+    if (s16) {
+      const int kp = s16_kpad(din);
+      HIP_OK(h, launch_split_rows(x, din, (int)rows, din, kp, h->x16.as<uint16_t>(), h->eflag.as<int32_t>(), s));
+      HIP_OK(h, launch_input_proj_s16(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
+                                      h->W + h->L.enc_bias[l], h->gin.as<float>(), s));
+    } else {
+      HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
+                                  h->gin.as<float>(), s));
+    }
     }
     const int residual = (h->cfg.residual && l > 0) ? 1 : 0;
     // layer 0 has no residual input: pass an internal pointer so a graph never bakes in the

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define CASR_DEV __device__ __forceinline__
 
@@ -12,6 +13,58 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 CASR_DEV f32x4 mfma16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
+
+// ---- split-f16 ("s16x3") fp32 contraction on the f16 MFMA pipes (2.5 PF dense vs 157 TF f32).
+// x = hi + 2^-11 lo with hi = f16_rn(x) and lo = f16_rn((x - hi) * 2^11): x - hi is exact in
+// f32 and the 2^11 scale keeps lo a normal f16, so hi:lo carries 22 significant bits.
+//   a.b = hi_a.hi_b + 2^-11 (hi_a.lo_b + lo_a.hi_b)   (+ the dropped 2^-22 lo.lo term)
+// with every f16 x f16 product exact and accumulated in f32 by v_mfma_f32_16x16x32_f16.
+// Measured on MI355X (tools/probes/split16_probe.hip, error / sum|a_k b_k| vs fp64): 8.8e-8 max,
+// against 2.6e-7 for the exact-f32 MFMA k-ordered chain on the same operands.  Operands must
+// stay below 65504 in magnitude (f16 range); the host rejects weights beyond 2^14.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr float S16_LO_SCALE = 2048.0f;
+constexpr float S16_LO_INV = 1.0f / 2048.0f;
+
+// v_mfma_f32_16x16x32_f16: lane l supplies A[l&15][k = 8(l>>4) + e] and B[k][l&15] for e = 0..7;
+// C/D as mfma16x16x4.
+CASR_DEV f32x4 mfma16x16x32h(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// hi / lo halves of one f32 packed as (hi | lo << 16); a non-finite x keeps hi = f16(x) and
+// lo = 0 so bit 30 (lo's exponent MSB, 0 whenever |lo| < 2) stays free for hand-off tags
+CASR_DEV uint32_t split16_word(float x) {
+  const _Float16 hi = (_Float16)x;
+  const float r = (x - (float)hi) * S16_LO_SCALE;
+  const _Float16 lo = (r == r && fabsf(r) < 65504.f) ? (_Float16)r : (_Float16)0.f;
+  return (uint32_t)__builtin_bit_cast(uint16_t, hi) | ((uint32_t)__builtin_bit_cast(uint16_t, lo) << 16);
+}
+
+// 8 split words (two u32x4) -> the 8-wide hi and lo MFMA operands
+CASR_DEV void unpack16(u32x4 w0, u32x4 w1, f16x8& hi, f16x8& lo) {
+  u32x4 h, l;
+  h.x = __builtin_amdgcn_perm(w0.y, w0.x, 0x05040100u);
+  h.y = __builtin_amdgcn_perm(w0.w, w0.z, 0x05040100u);
+  h.z = __builtin_amdgcn_perm(w1.y, w1.x, 0x05040100u);
+  h.w = __builtin_amdgcn_perm(w1.w, w1.z, 0x05040100u);
+  l.x = __builtin_amdgcn_perm(w0.y, w0.x, 0x07060302u);
+  l.y = __builtin_amdgcn_perm(w0.w, w0.z, 0x07060302u);
+  l.z = __builtin_amdgcn_perm(w1.y, w1.x, 0x07060302u);
+  l.w = __builtin_amdgcn_perm(w1.w, w1.z, 0x07060302u);
+  hi = __builtin_bit_cast(f16x8, h);
+  lo = __builtin_bit_cast(f16x8, l);
+}
+
+// three MFMAs of one s16x3 product into the (hi.hi, cross) accumulator pair
+CASR_DEV void mfma_s16(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x4& hh, f32x4& x) {
+  hh = mfma16x16x32h(ah, bh, hh);
+  x = mfma16x16x32h(ah, bl, x);
+  x = mfma16x16x32h(al, bh, x);
+}
+
+CASR_DEV float s16_combine(float hh, float x) { return hh + x * S16_LO_INV; }
 
 CASR_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 

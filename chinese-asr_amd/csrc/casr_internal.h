@@ -33,6 +33,7 @@ constexpr int CASR_DEV_BAD_CAND = 8;     // beam candidate index not in [0, k*V)
 constexpr int CASR_DEV_BAD_BACKPTR = 16; // back-pointer walk left [0, k)
 constexpr int CASR_DEV_REC_TIMEOUT = 32; // persistent recurrence: a bounded hand-off wait expired
 constexpr int CASR_DEV_BAD_AUDIO = 64;   // front-end: n_samples < 513 (torch.stft raises) or > n_max
+constexpr int CASR_DEV_F16_RANGE = 128;  // s16x3 path: a finite operand beyond the f16 range (>= 65520)
 
 // MFMA-fragment-major weight block: a 16-row x 64-k tile stored as [q=0..3][lane][4] so
 // lane l reads row (l&15), k = 16*(l>>4) + 4q + e with one coalesced 16 B load per q.
@@ -52,6 +53,10 @@ struct Layout {
   size_t b_attn;                     // [A]
   size_t w_hidden;                   // [HD][A]
   size_t v;                          // [A]
+  size_t info;                       // [64]: info[0] = 1 when the s16x3 images are valid
+  // s16x3 images (casr_common.h split16) of the MFMA operands, same float count as the f32 ones
+  size_t enc_wih16[CASR_MAX_LAYERS]; // [2*4H][Kp/32][32 hi | 32 lo], Kp = Din rounded up to 32
+  size_t enc_whh16[CASR_MAX_LAYERS]; // s16 frag-major [2][H/16][4][H/64] (recurrence.hip)
   size_t total;
   int layers, V, VP;
 };
@@ -165,6 +170,12 @@ hipError_t launch_gather_utts(const float* const* ptrs, const int32_t* lens, int
 // encoder.hip
 hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, const float* bias,
                              float* Gin, hipStream_t s);
+// s16x3 input projection: X16 / W16 are s16 row images with Kp (multiple of 32) k per row
+hipError_t launch_input_proj_s16(const float* X16, int M, int Kp, const float* W16, const float* bias,
+                                 float* Gin, hipStream_t s);
+hipError_t launch_split_rows(const float* X, int ldx, int M, int K, int Kp, uint16_t* out, int32_t* err,
+                             hipStream_t s);
+inline int s16_kpad(int K) { return (K + 31) / 32 * 32; }
 hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
                            const float* hprev, float* hnext, float* cst, float* hfin,
                            const int32_t* lens, int B, int Tp, int step, int residual, int row0,

@@ -71,7 +71,12 @@ inline TileOrder tile_order(int NB, int NM, int K) {
   return TileOrder{NB, NM, NG};
 }
 
-template <class Epi>
+// S16 = true: A and W are s16 row images (casr_common.h split16): row r holds K/32 k-tiles of
+// 128 B = [32 hi halves | 32 lo halves], so one k-tile of a row is the same 128 B the f32 kernel
+// stages (lda / ldw count 4-B words, K % 32 == 0) and the staging code is shared unchanged.
+// Lane (r, g) reads chunk g (hi, k = 8g..8g+7) and chunk 4 + g (lo) of each row and issues the
+// three f16 MFMAs of the s16x3 product per 16x16 tile.
+template <class Epi, bool S16 = false>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict__ Amat, int lda,
                                                       const float* __restrict__ Wmat, int ldw,
                                                       int M, int N, int K, TileOrder order, Epi epi) {
@@ -130,9 +135,36 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
       *reinterpret_cast<float4*>(la + TILE) = vw;
     }
   };
+  f32x4 accx[S16 ? 4 : 1][S16 ? 4 : 1];  // s16x3 cross-term accumulators
+  if constexpr (S16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) accx[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   auto compute = [&](const float* src) {
     const float* as = src;
     const float* ws = src + TILE;
+    if constexpr (S16) {
+      f16x8 ah[4], al[4], wh[4], wl[4];
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) {
+        const int row = wm * 64 + tm * 16 + r, sw = (row >> 1) & 7;
+        ah[tm] = *reinterpret_cast<const f16x8*>(as + row * GB_K + ((g ^ sw) << 2));
+        al[tm] = *reinterpret_cast<const f16x8*>(as + row * GB_K + (((4 + g) ^ sw) << 2));
+      }
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) {
+        const int row = wn * 64 + tn * 16 + r, sw = (row >> 1) & 7;
+        wh[tn] = *reinterpret_cast<const f16x8*>(ws + row * GB_K + ((g ^ sw) << 2));
+        wl[tn] = *reinterpret_cast<const f16x8*>(ws + row * GB_K + (((4 + g) ^ sw) << 2));
+      }
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) mfma_s16(ah[tm], al[tm], wh[tn], wl[tn], acc[tm][tn], accx[tm][tn]);
+      return;
+    }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int c = g * 2 + half;  // logical chunk of k = 8g + 4 half (same k order as the MFMA)
@@ -178,6 +210,14 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
     __syncthreads();
     compute(buf0);
     __syncthreads();
+  }
+  if constexpr (S16) {
+#pragma unroll
+    for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[tm][tn][e] = s16_combine(acc[tm][tn][e], accx[tm][tn][e]);
   }
 
   if constexpr (Epi::kRowTile) {
@@ -233,6 +273,61 @@ hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, con
   const TileOrder order = tile_order(N / GB_N, (M + GB_M - 1) / GB_M, Din);
   hipLaunchKernelGGL(gemm_nt_kernel<StoreBiasEpi>, dim3(order.blocks()), dim3(256), 0, s, X, Din, W,
                      Din, M, N, Din, order, epi);
+  return hipGetLastError();
+}
+
+hipError_t launch_input_proj_s16(const float* X16, int M, int Kp, const float* W16, const float* bias,
+                                 float* Gin, hipStream_t s) {
+  const int N = 8 * H;
+  if (Kp % GB_K != 0 || M <= 0) return hipErrorInvalidValue;
+  StoreBiasEpi epi{Gin, bias, N};
+  const TileOrder order = tile_order(N / GB_N, (M + GB_M - 1) / GB_M, Kp);
+  hipLaunchKernelGGL((gemm_nt_kernel<StoreBiasEpi, true>), dim3(order.blocks()), dim3(256), 0, s, X16, Kp, W16,
+                     Kp, M, N, Kp, order, epi);
+  return hipGetLastError();
+}
+
+// f32 rows [M][K] (stride ldx) -> s16 row images [M][Kp/32][32 hi | 32 lo] (zeros past K).
+// One thread per 8 consecutive k: two 16-B stores.  Raises CASR_DEV_F16_RANGE for a finite
+// element beyond the f16 range (its hi would be infinite).
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ X, int ldx, int M, int K,
+                                                         int Kp, uint16_t* __restrict__ out,
+                                                         int32_t* __restrict__ err) {
+  const int ng = Kp / 8;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)M * ng) return;
+  const int row = (int)(i / ng), q = (int)(i - (size_t)row * ng), k0 = q * 8;
+  float v[8];
+  const float* xp = X + (size_t)row * ldx + k0;
+  if (k0 + 8 <= K && (ldx & 3) == 0) {
+    const float4 a = *reinterpret_cast<const float4*>(xp), b = *reinterpret_cast<const float4*>(xp + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = k0 + e < K ? xp[e] : 0.f;
+  }
+  u32x4 hv, lv;
+  bool range_ok = true;
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const uint32_t w0 = split16_word(v[e]), w1 = split16_word(v[e + 1]);
+    const float m = fmaxf(fabsf(v[e]), fabsf(v[e + 1]));  // f16_rn overflows from 65520 on
+    range_ok &= !(m >= 65520.f && m < INFINITY);
+    hv[e / 2] = __builtin_amdgcn_perm(w1, w0, 0x05040100u);
+    lv[e / 2] = __builtin_amdgcn_perm(w1, w0, 0x07060302u);
+  }
+  if (!range_ok) __hip_atomic_fetch_or(err, CASR_DEV_F16_RANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint16_t* op = out + (size_t)row * Kp * 2 + (k0 / 32) * 64 + (k0 % 32);
+  *reinterpret_cast<u32x4*>(op) = hv;
+  *reinterpret_cast<u32x4*>(op + 32) = lv;
+}
+
+hipError_t launch_split_rows(const float* X, int ldx, int M, int K, int Kp, uint16_t* out, int32_t* err,
+                             hipStream_t s) {
+  if (M <= 0 || Kp % 32 != 0 || K > Kp) return hipErrorInvalidValue;
+  const size_t n = (size_t)M * (Kp / 8);
+  hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, X, ldx, M, K, Kp, out,
+                     err);
   return hipGetLastError();
 }
 

@@ -43,8 +43,6 @@ namespace {
 constexpr int NKC = H / 64;            // 4 k-chunks of 64 hidden units
 constexpr uint64_t SPIN_TICKS = 200000000ull;  // s_memrealtime runs at 100 MHz: 2 s
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
 constexpr uint32_t TAG_BIT = 0x40000000u;
 constexpr uint32_t NONFINITE = 0x3FFFFFFFu;
 

@@ -177,6 +177,18 @@ int casr_device_flags(casr_handle* h, int32_t* flags_host, void* stream);
  * launches always.  Both give bitwise identical results. */
 int casr_set_persistent(casr_handle* h, int enable);
 
+/* Arithmetic of the MFMA contractions (encoder input projection and recurrence; decoder LSTM
+ * cell and projection).  Both compute in f32 on f32 data and keep f32 accumulators:
+ *   CASR_PREC_F32    v_mfma_f32_16x16x4_f32, exact f32 products in k order;
+ *   CASR_PREC_S16X3  every f32 operand split as hi + 2^-11 lo (two f16), three f16 MFMAs per
+ *                    product (hi.hi + 2^-11 (hi.lo + lo.hi)) on the 16x-faster f16 pipes; 22
+ *                    significant operand bits, measured error no larger than the f32 path's.
+ * Default S16X3.  A blob whose MFMA weights do not fit the f16 range (|w| >= 2^14 or
+ * non-finite) runs F32 whatever is set; casr_get_precision reports the effective mode. */
+enum { CASR_PREC_F32 = 0, CASR_PREC_S16X3 = 1 };
+int casr_set_precision(casr_handle* h, int precision);
+int casr_get_precision(const casr_handle* h); /* effective mode, -1 on a NULL handle */
+
 /* Which recurrence casr_encode would use for batch B: 1 persistent, 0 per-step, -1 bad args. */
 int casr_recurrence_mode(const casr_handle* h, int B);
 

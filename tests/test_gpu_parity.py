@@ -1,6 +1,9 @@
 """HIP path vs the reference (golden vectors) and vs the CPU oracle, through the C ABI.
 
-Tolerances (fp32 everywhere; differences come only from summation order / libm ulps):
+Every test runs twice, once per MFMA arithmetic (s16x3 split-f16 and exact f32; the eng
+fixture).  Tolerances (f32 data and accumulators everywhere; differences come only from
+summation order, operand splitting (s16x3: 22-bit operands, measured error below the f32
+chain's) and libm ulps):
   features 2e-5 abs, encoder outputs 1e-4 abs, beam / greedy scores 2e-3 abs (sums of up to
   40 log-probs of magnitude <= ~40), attention weights 1e-5 abs; token ids must be identical.
 """
@@ -23,10 +26,14 @@ CFG = CasrConfig()
 FRAMES = golden_frames(META)
 
 
-@pytest.fixture(scope="module")
-def eng():
+@pytest.fixture(scope="module", params=["s16x3", "f32"])
+def eng(request):
+    """One handle per MFMA arithmetic (include/casr.h casr_set_precision): every parity test
+    runs on both the split-f16 path (default) and the exact-f32 path."""
     from casr.engine import Engine
     e = Engine(CFG, *synthetic_state_dicts(CFG, peaked=False))
+    e.set_precision(request.param)
+    assert e.precision() == request.param
     yield e
     e.close()
 
