@@ -544,6 +544,7 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
     // layer 0 has no residual input: pass an internal pointer so a graph never bakes in the
     // caller's feature buffer
     const float* xin = residual ? x : out;
+    const float* whh = h->W + (s16 ? h->L.enc_whh16[l] : h->L.enc_whh[l]);
     if (persistent) {
       // one launch runs all Tp steps; h and c start at zero inside (util.py:1236-1247)
       HIP_OK(h, reset_rec_layer(reinterpret_cast<uint32_t*>(h->hx.p), B, s));
@@ -557,9 +558,9 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
       }
       {
         ProfScope ps(&h->prof, CASR_K_REC_STEP, s);
-        HIP_OK(h, launch_rec_layer(h->W + h->L.enc_whh[l], h->gin.as<float>(), xin, out,
+        HIP_OK(h, launch_rec_layer(whh, h->gin.as<float>(), xin, out,
                                    reinterpret_cast<uint32_t*>(h->hx.p), h->hfin.as<float>(),
-                                   h->cst.as<float>(), dl, B, Tp, residual, h->eflag.as<int32_t>(),
+                                   h->cst.as<float>(), dl, B, Tp, residual, s16, h->eflag.as<int32_t>(),
                                    tbuf.as<uint32_t>(), s));
       }
       if (trace_path) {
@@ -586,8 +587,8 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
         const float* hprev = hb + (size_t)(step & 1) * 2 * B * H;
         float* hnext = hb + (size_t)((step + 1) & 1) * 2 * B * H;
         ProfScope ps(prof, CASR_K_REC_STEP, st);
-        e = launch_rec_step(h->W + h->L.enc_whh[l], h->gin.as<float>(), xin, out, hprev, hnext,
-                            h->cst.as<float>(), h->hfin.as<float>(), dl, B, Tp, step, residual, r0, r1, st);
+        e = launch_rec_step(whh, h->gin.as<float>(), xin, out, hprev, hnext,
+                            h->cst.as<float>(), h->hfin.as<float>(), dl, B, Tp, step, residual, r0, r1, s16, st);
       }
       return e;
     };
@@ -600,7 +601,7 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
       for (int p = 0; p < nsplit; ++p) {
         const int r0 = (nsplit == 1 || p == 0) ? 0 : half;
         const int r1 = (nsplit == 1 || p == 1) ? B : half;
-        const std::vector<uint64_t> key = {1, (uint64_t)l, (uint64_t)B, (uint64_t)Tp, (uint64_t)residual,
+        const std::vector<uint64_t> key = {1, (uint64_t)s16, (uint64_t)l, (uint64_t)B, (uint64_t)Tp, (uint64_t)residual,
                                            (uint64_t)r0, (uint64_t)r1, (uint64_t)h->W, (uint64_t)h->gin.p,
                                            (uint64_t)xin, (uint64_t)out, (uint64_t)hb, (uint64_t)h->cst.p,
                                            (uint64_t)h->hfin.p, (uint64_t)dl};

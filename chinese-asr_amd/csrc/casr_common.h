@@ -57,6 +57,14 @@ CASR_DEV void unpack16(u32x4 w0, u32x4 w1, f16x8& hi, f16x8& lo) {
   lo = __builtin_bit_cast(f16x8, l);
 }
 
+// unpack16 of hand-off words whose bit 30 (lo's exponent MSB) carries a tag: cleared here
+CASR_DEV void unpack16_tagged(u32x4 w0, u32x4 w1, f16x8& hi, f16x8& lo) {
+  unpack16(w0, w1, hi, lo);
+  u32x4 l = __builtin_bit_cast(u32x4, lo);
+  l &= 0xBFFFBFFFu;
+  lo = __builtin_bit_cast(f16x8, l);
+}
+
 // three MFMAs of one s16x3 product into the (hi.hi, cross) accumulator pair
 CASR_DEV void mfma_s16(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x4& hh, f32x4& x) {
   hh = mfma16x16x32h(ah, bh, hh);

@@ -179,7 +179,7 @@ inline int s16_kpad(int K) { return (K + 31) / 32 * 32; }
 hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
                            const float* hprev, float* hnext, float* cst, float* hfin,
                            const int32_t* lens, int B, int Tp, int step, int residual, int row0,
-                           int row1, hipStream_t s);
+                           int row1, int s16, hipStream_t s);
 // recurrence.hip: persistent per-layer recurrence (all Tp steps in one launch)
 size_t rec_layer_granule_bytes(int B);
 int rec_layer_grid_blocks(int B);
@@ -188,7 +188,7 @@ hipError_t rec_layer_occupancy(int* blocks_per_cu);
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s);  // before EVERY launch_rec_layer
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
-                            int residual, int32_t* err, uint32_t* trace, hipStream_t s);
+                            int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s);
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s);
 

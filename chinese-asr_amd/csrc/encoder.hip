@@ -344,6 +344,9 @@ hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, cons
 
 // ------------------------------------------------------------------ recurrence step
 // grid (H/16 unit blocks, ceil(B/16) row blocks, 2 directions), block 256.
+// S16: s16 W_hh image and s16x3 MFMAs, the h operand split in registers by the same
+// split16_word the persistent kernel's producers apply (so both paths give the same bits).
+template <bool S16>
 __global__ __launch_bounds__(256) void rec_step_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, const float* __restrict__ hprev, float* __restrict__ hnext,
@@ -393,6 +396,29 @@ __global__ __launch_bounds__(256) void rec_step_kernel(
 #pragma unroll
       for (int q = 0; q < 4; ++q) bw[tn][q] = *reinterpret_cast<const float4*>(wb + q * 256);
     }
+    if constexpr (S16) {
+      // unit 16g + 8j + e of the chunk: a[2j] / a[2j + 1] hold e = 0..3 / 4..7
+      f32x4 accx[4];
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) accx[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float4 p = a[2 * j], q = a[2 * j + 1];
+        const u32x4 w0 = {split16_word(p.x), split16_word(p.y), split16_word(p.z), split16_word(p.w)};
+        const u32x4 w1 = {split16_word(q.x), split16_word(q.y), split16_word(q.z), split16_word(q.w)};
+        f16x8 ah, al;
+        unpack16(w0, w1, ah, al);
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn)
+          mfma_s16(ah, al, __builtin_bit_cast(f16x8, bw[tn][2 * j]), __builtin_bit_cast(f16x8, bw[tn][2 * j + 1]),
+                   acc[tn], accx[tn]);
+      }
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[tn][e] = s16_combine(acc[tn][e], accx[tn][e]);
+      continue;
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -428,10 +454,14 @@ __global__ __launch_bounds__(256) void rec_step_kernel(
 hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
                            const float* hprev, float* hnext, float* cst, float* hfin,
                            const int32_t* lens, int B, int Tp, int step, int residual, int row0, int row1,
-                           hipStream_t s) {
+                           int s16, hipStream_t s) {
   dim3 grid(H / 16, (row1 - row0 + 15) / 16, 2);
-  hipLaunchKernelGGL(rec_step_kernel, grid, dim3(256), 0, s, Whh_f, Gin, xin, out, hprev, hnext,
-                     cst, hfin, lens, B, Tp, step, residual, row0, row1);
+  if (s16)
+    hipLaunchKernelGGL(rec_step_kernel<true>, grid, dim3(256), 0, s, Whh_f, Gin, xin, out, hprev, hnext,
+                       cst, hfin, lens, B, Tp, step, residual, row0, row1);
+  else
+    hipLaunchKernelGGL(rec_step_kernel<false>, grid, dim3(256), 0, s, Whh_f, Gin, xin, out, hprev, hnext,
+                       cst, hfin, lens, B, Tp, step, residual, row0, row1);
   return hipGetLastError();
 }
 

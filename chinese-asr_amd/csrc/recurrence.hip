@@ -46,9 +46,19 @@ constexpr uint64_t SPIN_TICKS = 200000000ull;  // s_memrealtime runs at 100 MHz:
 constexpr uint32_t TAG_BIT = 0x40000000u;
 constexpr uint32_t NONFINITE = 0x3FFFFFFFu;
 
+// S16: the granule is the s16 split word of h (casr_common.h split16_word: hi | lo << 16).  |h| <=
+// 1 keeps |lo| < 2, so bit 30 (lo's exponent MSB) is free for the tag here too; a non-finite h
+// travels as hi = f16(h) (NaN) with lo = 0.  The consumer masks the tag and feeds the halves to
+// the f16 MFMAs directly.
+template <bool S16>
 CASR_DEV void store_granule(uint32_t* p, int step_tagged, float v) {
-  uint32_t x = __float_as_uint(v);
-  if (!(fabsf(v) < 2.0f)) x = NONFINITE;
+  uint32_t x;
+  if constexpr (S16) {
+    x = split16_word(v);
+  } else {
+    x = __float_as_uint(v);
+    if (!(fabsf(v) < 2.0f)) x = NONFINITE;
+  }
   x |= (step_tagged & 1) ? TAG_BIT : 0u;
   __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dword sc1
 }
@@ -59,7 +69,11 @@ CASR_DEV float decode_granule(uint32_t x) {
 }
 
 // RG batch rows per workgroup (32: 8 waves, one workgroup per CU; 16: 4 waves, two per CU)
-template <int RG>
+// S16: W_hh is the s16 fragment image (casr_capi.hip pack_frag16) and the contraction runs as
+// s16x3 on v_mfma_f32_16x16x32_f16 (2 k-steps of 32 per 64-unit chunk, 24 MFMAs per wave and
+// step instead of 64 f32 ones at twice the cycles each).  Lane (r, g) of k-step j covers units
+// 16g + 8j + e of its chunk: exactly the granule words its sweep already loaded.
+template <int RG, bool S16>
 __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, uint32_t* __restrict__ hx, float* __restrict__ hfin,
@@ -96,6 +110,7 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) bw[tn][q] = *reinterpret_cast<const float4*>(wb + q * 256);
   }
+  // S16 view of the same registers: bw[tn][2j + hl] = the 8 halves of k-step j (hl 0 hi, 1 lo)
   // granule sweep of this wave: rows (lane & 15) of its half, units kc*64 + (lane>>4)*16 + 0..15;
   // the buffer descriptor takes the wave-uniform part, the lane part is the byte voffset
   const int wbase = __builtin_amdgcn_readfirstlane(((d * Bp + rg * RG + half * 16) * H + kc * 64));
@@ -158,16 +173,35 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
       }
       if (tr && lane == 0) tr[s * 5 + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
       load_operands(s + 1, gin_n, x_n);
+      if constexpr (S16) {
+        f32x4 accx[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float a0 = decode_granule(v[q].x), a1 = decode_granule(v[q].y);
-        const float a2 = decode_granule(v[q].z), a3 = decode_granule(v[q].w);
+        for (int tn = 0; tn < 4; ++tn) accx[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int tn = 0; tn < 4; ++tn) {
-          acc[tn] = mfma16x16x4(a0, bw[tn][q].x, acc[tn]);
-          acc[tn] = mfma16x16x4(a1, bw[tn][q].y, acc[tn]);
-          acc[tn] = mfma16x16x4(a2, bw[tn][q].z, acc[tn]);
-          acc[tn] = mfma16x16x4(a3, bw[tn][q].w, acc[tn]);
+        for (int j = 0; j < 2; ++j) {
+          f16x8 ah, al;
+          unpack16_tagged(v[2 * j], v[2 * j + 1], ah, al);
+#pragma unroll
+          for (int tn = 0; tn < 4; ++tn)
+            mfma_s16(ah, al, __builtin_bit_cast(f16x8, bw[tn][2 * j]), __builtin_bit_cast(f16x8, bw[tn][2 * j + 1]),
+                     acc[tn], accx[tn]);
+        }
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[tn][e] = s16_combine(acc[tn][e], accx[tn][e]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float a0 = decode_granule(v[q].x), a1 = decode_granule(v[q].y);
+          const float a2 = decode_granule(v[q].z), a3 = decode_granule(v[q].w);
+#pragma unroll
+          for (int tn = 0; tn < 4; ++tn) {
+            acc[tn] = mfma16x16x4(a0, bw[tn][q].x, acc[tn]);
+            acc[tn] = mfma16x16x4(a1, bw[tn][q].y, acc[tn]);
+            acc[tn] = mfma16x16x4(a2, bw[tn][q].z, acc[tn]);
+            acc[tn] = mfma16x16x4(a3, bw[tn][q].w, acc[tn]);
+          }
         }
       }
     } else {
@@ -201,7 +235,7 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
       if (s == len - 1) hfin[si] = h2;
       out[oi] = residual ? (h2 + x_res) : h2;
     }
-    if (s + 1 < tmax) store_granule(hx + (size_t)((s + 1) % 3) * 2 * plane + gi, s + 1, h2);
+    if (s + 1 < tmax) store_granule<S16>(hx + (size_t)((s + 1) % 3) * 2 * plane + gi, s + 1, h2);
     if (tr && lane == 0) {
       tr[s * 5 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
       tr[s * 5 + 4] = npass;
@@ -233,9 +267,16 @@ int rec_layer_waves() { return rec_rg() / 4; }
 int rec_layer_grid_blocks(int B) { return (H / 16) * ((B + rec_rg() - 1) / rec_rg()) * 2; }
 
 hipError_t rec_layer_occupancy(int* blocks_per_cu) {
-  return rec_rg() == 16
-             ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rec_layer_kernel<16>, 256, 0)
-             : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, rec_layer_kernel<32>, 512, 0);
+  // both arithmetic variants must fit: the capacity is the smaller of the two
+  int a = 0, b = 0;
+  hipError_t e = rec_rg() == 16
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rec_layer_kernel<16, false>, 256, 0)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rec_layer_kernel<32, false>, 512, 0);
+  if (e == hipSuccess)
+    e = rec_rg() == 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rec_layer_kernel<16, true>, 256, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rec_layer_kernel<32, true>, 512, 0);
+  *blocks_per_cu = a < b ? a : b;
+  return e;
 }
 
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
@@ -248,16 +289,18 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
 
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
-                            int residual, int32_t* err, uint32_t* trace, hipStream_t s) {
+                            int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s) {
   const int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for either RG
   const int RG = rec_rg();
   dim3 grid(H / 16, (B + RG - 1) / RG, 2);
+  auto go = [&](auto kern, int threads) {
+    hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens, B, Bp, Tp,
+                       residual, err, trace);
+  };
   if (RG == 16)
-    hipLaunchKernelGGL(rec_layer_kernel<16>, grid, dim3(256), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens,
-                       B, Bp, Tp, residual, err, trace);
+    s16 ? go(rec_layer_kernel<16, true>, 256) : go(rec_layer_kernel<16, false>, 256);
   else
-    hipLaunchKernelGGL(rec_layer_kernel<32>, grid, dim3(512), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens,
-                     B, Bp, Tp, residual, err, trace);
+    s16 ? go(rec_layer_kernel<32, true>, 512) : go(rec_layer_kernel<32, false>, 512);
   return hipGetLastError();
 }
 
