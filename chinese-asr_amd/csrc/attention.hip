@@ -240,9 +240,12 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     const float4 p1 = *reinterpret_cast<const float4*>(xs + (1 * KPB + j) * C + 4 * c4);
     const float4 p2 = *reinterpret_cast<const float4*>(xs + (2 * KPB + j) * C + 4 * c4);
     const float4 p3 = *reinterpret_cast<const float4*>(xs + (3 * KPB + j) * C + 4 * c4);
-    *reinterpret_cast<float4*>(st + (row0 + j) * ST + 4 * c4) =
-        make_float4((p0.x + p1.x) + (p2.x + p3.x), (p0.y + p1.y) + (p2.y + p3.y),
-                    (p0.z + p1.z) + (p2.z + p3.z), (p0.w + p1.w) + (p2.w + p3.w));
+    const float4 cv = make_float4((p0.x + p1.x) + (p2.x + p3.x), (p0.y + p1.y) + (p2.y + p3.y),
+                                  (p0.z + p1.z) + (p2.z + p3.z), (p0.w + p1.w) + (p2.w + p3.w));
+    *reinterpret_cast<float4*>(st + (row0 + j) * ST + 4 * c4) = cv;
+    // the s16 split words of ctx for the next step's decoder GEMMs (casr_internal.h ST16)
+    *reinterpret_cast<u32x4*>(st + (row0 + j) * ST + ST16 + 4 * c4) =
+        u32x4{split16_word(cv.x), split16_word(cv.y), split16_word(cv.z), split16_word(cv.w)};
   }
 }
 

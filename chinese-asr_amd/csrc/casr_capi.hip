@@ -49,6 +49,9 @@ Layout make_layout(const casr_config& cfg) {
     L.enc_wih16[l] = take((size_t)8 * H * s16_kpad(din));
     L.enc_whh16[l] = take((size_t)2 * 4 * H * H);
   }
+  L.emb16 = take((size_t)cfg.vocab * E);
+  L.dec_w16 = take((size_t)4 * HD * KDEC);
+  L.proj_w16 = take((size_t)L.VP * KPROJ);
   L.total = off;
   return L;
 }
@@ -299,6 +302,10 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
           (!in_range(w->enc_w_ih[l][d], (size_t)4 * H * (l == 0 ? D : C)) ||
            !in_range(w->enc_w_hh[l][d], (size_t)4 * H * H)))
         s16_ok = false;
+  if (w->embedding && w->dec_w_ih && w->dec_w_hh && w->proj_w &&
+      (!in_range(w->embedding, (size_t)cfg->vocab * E) || !in_range(w->dec_w_ih, (size_t)4 * HD * (E + C)) ||
+       !in_range(w->dec_w_hh, (size_t)4 * HD * HD) || !in_range(w->proj_w, (size_t)cfg->vocab * KPROJ)))
+    s16_ok = false;
   std::memset(out, 0, L.total * sizeof(float));
   out[L.info] = s16_ok ? 1.f : 0.f;
   const int V = cfg->vocab;
@@ -335,20 +342,28 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
       !w->proj_b || !w->attn_w_enc || !w->attn_b || !w->attn_w_hidden || !w->attn_v)
     return fail(nullptr, CASR_ERR_ARG, "decoder/attention: NULL tensor");
   std::memcpy(out + L.emb, w->embedding, sizeof(float) * (size_t)V * E);
+  {
+    uint16_t* e16 = reinterpret_cast<uint16_t*>(out + L.emb16);
+    for (size_t i = 0; i < (size_t)V * E; ++i) split16_host(w->embedding[i], e16[2 * i], e16[2 * i + 1]);
+  }
   // decoder LSTM: K order [emb | ctx | h] = [W_ih | W_hh]
-  pack_frag(out + L.dec_w, 4 * HD / 16, KDEC / 64, [&](int n, int k) {
+  auto decw = [&](int n, int k) {
     const int jb = n / 64, g = (n / 16) % 4, u = jb * 16 + (n % 16);
     const int orow = g * HD + u;
     return k < E + C ? w->dec_w_ih[(size_t)orow * (E + C) + k] : w->dec_w_hh[(size_t)orow * HD + (k - E - C)];
-  });
+  };
+  pack_frag(out + L.dec_w, 4 * HD / 16, KDEC / 64, decw);
+  pack_frag16(out + L.dec_w16, 4 * HD / 16, KDEC / 64, decw);
   for (int g = 0; g < 4; ++g)
     for (int u = 0; u < HD; ++u)
       out[L.dec_b + packed_gate_row(g, u)] = w->dec_b_ih[g * HD + u] + w->dec_b_hh[g * HD + u];
   // projection: reference input is cat([h, ctx]) (decoder.py:131); packed K order [ctx | h]
-  pack_frag(out + L.proj_w, L.VP / 16, KPROJ / 64, [&](int n, int k) {
+  auto projw = [&](int n, int k) {
     if (n >= V) return 0.f;
     return k < C ? w->proj_w[(size_t)n * KPROJ + HD + k] : w->proj_w[(size_t)n * KPROJ + (k - C)];
-  });
+  };
+  pack_frag(out + L.proj_w, L.VP / 16, KPROJ / 64, projw);
+  pack_frag16(out + L.proj_w16, L.VP / 16, KPROJ / 64, projw);
   for (int n = 0; n < V; ++n) out[L.proj_b + n] = w->proj_b[n];
   for (int a = 0; a < A; ++a)
     for (int c = 0; c < C; ++c) out[L.wencT + (size_t)a * C + c] = w->attn_w_enc[(size_t)c * A + a];
@@ -709,6 +724,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   a.sos = h->cfg.sos;
   a.eos = h->cfg.eos;
   a.temperature = h->cfg.temperature;
+  a.s16 = h->s16() ? 1 : 0;
   a.prof = &h->prof;
   return CASR_OK;
 }
@@ -735,7 +751,7 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   float* ial = align ? iacc + B : nullptr;
   uint8_t* ifin = reinterpret_cast<uint8_t*>(iacc + B + nal);
   a.prof = nullptr;
-  const std::vector<uint64_t> key = {2, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
+  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
                                      (uint64_t)(align != nullptr), (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->enc_out, (uint64_t)h->keysT.p,
                                      (uint64_t)h->hfin.p, (uint64_t)h->cst.p, (uint64_t)h->lens.p};
@@ -773,7 +789,7 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
   uint32_t lmw, lw;
   std::memcpy(&lmw, &lm_weight, 4);
   std::memcpy(&lw, &length_weight, 4);
-  const std::vector<uint64_t> key = {3, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
+  const std::vector<uint64_t> key = {3, (uint64_t)a.s16, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
                                      (uint64_t)h->gout.p, (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->bp.p, (uint64_t)h->tk.p, (uint64_t)h->rec.p,
                                      (uint64_t)h->enc_out, (uint64_t)h->keysT.p, (uint64_t)h->hfin.p,

@@ -21,7 +21,8 @@ constexpr int E = 256;    // embedding
 constexpr int A = 128;    // attention size
 constexpr int KDEC = E + C + HD;  // 1280: decoder LSTM contraction [emb | ctx | h]
 constexpr int KPROJ = C + HD;     // 1024: projection contraction [ctx | h]
-constexpr int ST = C + HD + HD;   // 1536: per-row decoder state [ctx | h | c]
+constexpr int ST16 = C + HD + HD;  // offset of the s16 split words [ctx16 | h16] in a state row
+constexpr int ST = ST16 + C + HD;  // 2560: per-row decoder state [ctx | h | c | ctx16 | h16]
 constexpr int KMAX_BEAM = 16;
 
 // Device guard bits: a data-dependent index (token id, predecessor row, back-pointer) out of
@@ -57,6 +58,9 @@ struct Layout {
   // s16x3 images (casr_common.h split16) of the MFMA operands, same float count as the f32 ones
   size_t enc_wih16[CASR_MAX_LAYERS]; // [2*4H][Kp/32][32 hi | 32 lo], Kp = Din rounded up to 32
   size_t enc_whh16[CASR_MAX_LAYERS]; // s16 frag-major [2][H/16][4][H/64] (recurrence.hip)
+  size_t emb16;                      // [V][E] split words (split16_word)
+  size_t dec_w16;                    // s16 frag-major, same tiling / k order as dec_w
+  size_t proj_w16;                   // s16 frag-major, same tiling / k order as proj_w
   size_t total;
   int layers, V, VP;
 };
@@ -222,6 +226,7 @@ struct DecodeArgs {
   const int32_t* lens;   // [B]
   int B, Tp, k, V, max_len, sos, eos;
   float temperature;
+  int s16;               // decoder GEMMs on the s16x3 images (casr_set_precision)
   Profiler* prof;        // may be null
 };
 

@@ -61,7 +61,11 @@ __device__ __forceinline__ void lds_dma16(const float* src, float* lds_wave_base
 // alias the read and does not drain it with vmcnt(0) (one array with a runtime index did: the
 // prefetch was serialised).  Each lane's A source rows are resolved once before the loop (an
 // ordinary load beside in-flight DMA also forces vmcnt(0)).
-template <int WR, class ASrc, class Epi>
+// S16: A rows are split words (split16_word: [emb16 | ctx16 | h16]) and W is the s16 fragment
+// image (pack_frag16); a 64-deep tile is 2 k-steps of v_mfma_f32_16x16x32_f16 (s16x3), k-step
+// js = 2 kt + j going to wave kq = js % KQ.  Lane (r, g) of step j reads A words 16g + 8j .. +7
+// (two swizzled 16-B chunks) and W block [j][hi|lo][lane].
+template <int WR, class ASrc, class Epi, bool S16 = false>
 __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, const float* __restrict__ Wf,
                                                     ASrc asrc, Epi epi) {
   constexpr int KQ = 8 / WR, QPW = 4 / KQ, BM = 16 * WR, ATILE = BM * DG_BK;
@@ -101,13 +105,31 @@ __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, 
     }
   };
 
-  f32x4 acc[4];
+  f32x4 acc[4], accx[4];
 #pragma unroll
-  for (int tn = 0; tn < 4; ++tn) acc[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int tn = 0; tn < 4; ++tn) acc[tn] = accx[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int arow = ws * 16 + r;
-  auto compute = [&](const float* src) {
+  auto compute = [&](const float* src, int kt) {
     const float* la = src;
     const float* lw = src + ATILE;
+    if constexpr (S16) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if ((2 * kt + j) % KQ != kq) continue;
+        const int c0 = 4 * g + 2 * j;
+        const u32x4 w0 = *reinterpret_cast<const u32x4*>(la + arow * DG_BK + ((c0 ^ (arow & 15)) << 2));
+        const u32x4 w1 = *reinterpret_cast<const u32x4*>(la + arow * DG_BK + (((c0 + 1) ^ (arow & 15)) << 2));
+        f16x8 ah, al;
+        unpack16(w0, w1, ah, al);
+#pragma unroll
+        for (int tn = 0; tn < 4; ++tn) {
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(lw + tn * FRAG + (2 * j) * 256 + lane * 4);
+          const f16x8 bl = *reinterpret_cast<const f16x8*>(lw + tn * FRAG + (2 * j + 1) * 256 + lane * 4);
+          mfma_s16(ah, al, bh, bl, acc[tn], accx[tn]);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int qh = 0; qh < QPW; ++qh) {
       const int q = kq * QPW + qh;
@@ -128,12 +150,18 @@ __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, 
   __syncthreads();
   for (int kt = 0; kt < nkt; kt += 2) {
     if (kt + 1 < nkt) stage(buf1, kt + 1);
-    compute(buf0);
+    compute(buf0, kt);
     __syncthreads();  // retires this wave's DMA into buf1 and everyone's reads of buf0
     if (kt + 1 >= nkt) break;
     if (kt + 2 < nkt) stage(buf0, kt + 2);
-    compute(buf1);
+    compute(buf1, kt + 1);
     __syncthreads();
+  }
+  if constexpr (S16) {
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[tn][e] = s16_combine(acc[tn][e], accx[tn][e]);
   }
   // k slices 1..KQ-1 hand their partial sums to slice 0 through LDS (free after the last barrier)
   f32x4* part = reinterpret_cast<f32x4*>(buf0);
@@ -154,20 +182,30 @@ __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, 
 
 // 64-row blocks where that still gives >= 2 blocks per CU, else 32-row blocks
 template <class ASrc, class Epi>
-static void launch_dgemm(int NB, int R, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi, hipStream_t s) {
+static void launch_dgemm(int NB, int R, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi, int s16,
+                         hipStream_t s) {
   const int NR64 = (R + 63) / 64;
   if ((int)xcd_grid(NB, NR64) >= 512) {
-    hipLaunchKernelGGL((dgemm_kernel<4, ASrc, Epi>), dim3(xcd_grid(NB, NR64)), dim3(512), 0, s, NB, NR64, nkt, Wf,
-                       asrc, epi);
+    if (s16)
+      hipLaunchKernelGGL((dgemm_kernel<4, ASrc, Epi, true>), dim3(xcd_grid(NB, NR64)), dim3(512), 0, s, NB, NR64,
+                         nkt, Wf, asrc, epi);
+    else
+      hipLaunchKernelGGL((dgemm_kernel<4, ASrc, Epi, false>), dim3(xcd_grid(NB, NR64)), dim3(512), 0, s, NB, NR64,
+                         nkt, Wf, asrc, epi);
   } else {
     const int NR32 = (R + 31) / 32;
-    hipLaunchKernelGGL((dgemm_kernel<2, ASrc, Epi>), dim3(xcd_grid(NB, NR32)), dim3(512), 0, s, NB, NR32, nkt, Wf,
-                       asrc, epi);
+    if (s16)
+      hipLaunchKernelGGL((dgemm_kernel<2, ASrc, Epi, true>), dim3(xcd_grid(NB, NR32)), dim3(512), 0, s, NB, NR32,
+                         nkt, Wf, asrc, epi);
+    else
+      hipLaunchKernelGGL((dgemm_kernel<2, ASrc, Epi, false>), dim3(xcd_grid(NB, NR32)), dim3(512), 0, s, NB, NR32,
+                         nkt, Wf, asrc, epi);
   }
 }
 
 // A rows of the decoder LSTM: [embed(tok[r]) | st_old[src[r]][0:1024] = ctx | h]; a 64-deep
 // k tile lies in one segment (E = 256 is a multiple of 64).  Rows >= R read row R-1 (unused).
+// s16: emb is the split-word table (emb16) and the state segment starts at ST16 ([ctx16 | h16]).
 struct DecLstmA {
   static constexpr int kSeg = E;  // k < kSeg: embedding row, else state row
   const float* emb;
@@ -175,7 +213,7 @@ struct DecLstmA {
   const int32_t* tok;
   const int32_t* src;
   int32_t* err;
-  int R, V;
+  int R, V, s16;
   __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1) const {
     row = row < R ? row : R - 1;
     int t = tok[row];
@@ -184,7 +222,7 @@ struct DecLstmA {
       t = 0;
     }
     seg0 = emb + (size_t)t * E;
-    seg1 = st_old + (size_t)safe_src(row) * ST;
+    seg1 = st_old + (size_t)safe_src(row) * ST + (s16 ? ST16 : 0);
   }
   __device__ __forceinline__ int safe_src(int row) const {
     const int s = src[row];
@@ -220,16 +258,17 @@ struct DecLstmEpi {
                 st_old[(size_t)rows.safe_src(row) * ST + C + HD + U], h2, c2);
       st_new[(size_t)row * ST + C + U] = h2;
       st_new[(size_t)row * ST + C + HD + U] = c2;
+      reinterpret_cast<uint32_t*>(st_new)[(size_t)row * ST + ST16 + C + U] = split16_word(h2);
     }
   }
 };
 
-struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h]
+struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16: [ctx16 | h16])
   static constexpr int kSeg = 0;
   const float* st;
-  int R;
+  int R, s16;
   __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1) const {
-    seg0 = seg1 = st + (size_t)(row < R ? row : R - 1) * ST;
+    seg0 = seg1 = st + (size_t)(row < R ? row : R - 1) * ST + (s16 ? ST16 : 0);
   }
 };
 
@@ -261,7 +300,7 @@ __global__ void decode_init_kernel(float* __restrict__ st0, const float* __restr
                                    float* __restrict__ score) {
   const int r = blockIdx.x, b = r / k;
   float* o = st0 + (size_t)r * ST;
-  for (int i = threadIdx.x; i < ST; i += blockDim.x) {
+  for (int i = threadIdx.x; i < ST16; i += blockDim.x) {
     float v;
     if (i < C) {
       v = 0.f;
@@ -273,6 +312,7 @@ __global__ void decode_init_kernel(float* __restrict__ st0, const float* __restr
       v = cfin[((size_t)(u / H) * B + b) * H + (u % H)];
     }
     o[i] = v;
+    if (i < C + HD) reinterpret_cast<uint32_t*>(o)[ST16 + i] = split16_word(v);
   }
   if (threadIdx.x == 0) {
     tok[r] = sos;
@@ -685,9 +725,9 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   float* st_new = d.st[(l + 1) & 1];
   {
     ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
-    DecLstmA asrc{a.W + a.L.emb, st_old, d.tok[l & 1], d.src[l & 1], d.err, R, a.V};
+    DecLstmA asrc{a.W + (a.s16 ? a.L.emb16 : a.L.emb), st_old, d.tok[l & 1], d.src[l & 1], d.err, R, a.V, a.s16};
     DecLstmEpi epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, R, l, total};
-    launch_dgemm(HD / 16, R, KDEC / DG_BK, a.W + a.L.dec_w, asrc, epi, s);
+    launch_dgemm(HD / 16, R, KDEC / DG_BK, a.W + (a.s16 ? a.L.dec_w16 : a.L.dec_w), asrc, epi, a.s16, s);
   }
   hipError_t e;
   {
@@ -697,9 +737,9 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   if (e != hipSuccess) return e;
   {
     ProfScope ps(a.prof, CASR_K_PROJ, s);
-    ProjA asrc{st_new, R};
+    ProjA asrc{st_new, R, a.s16};
     ProjEpi epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total};
-    launch_dgemm(a.L.VP / 64, R, KPROJ / DG_BK, a.W + a.L.proj_w, asrc, epi, s);
+    launch_dgemm(a.L.VP / 64, R, KPROJ / DG_BK, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, s);
   }
   return hipGetLastError();
 }
