@@ -290,16 +290,17 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
   const Layout L = make_layout(*cfg);
   // the s16x3 images need every MFMA weight inside the f16 range with room to spare; blob word
   // L.info records whether they are usable (casr_bind_weights reads it)
-  auto in_range = [](const float* p, size_t n) {
+  // (the input projection's images need |w| < 16: gemm16.hip scales w_hi by 2^11 in f16)
+  auto in_range = [](const float* p, size_t n, float lim = 16384.f) {
     for (size_t i = 0; i < n; ++i)
-      if (!(std::fabs(p[i]) < 16384.f)) return false;
+      if (!(std::fabs(p[i]) < lim)) return false;
     return true;
   };
   bool s16_ok = true;
   for (int l = 0; l < cfg->enc_layers; ++l)
     for (int d = 0; d < 2; ++d)
       if (w->enc_w_ih[l][d] && w->enc_w_hh[l][d] &&
-          (!in_range(w->enc_w_ih[l][d], (size_t)4 * H * (l == 0 ? D : C)) ||
+          (!in_range(w->enc_w_ih[l][d], (size_t)4 * H * (l == 0 ? D : C), 16.f) ||
            !in_range(w->enc_w_hh[l][d], (size_t)4 * H * H)))
         s16_ok = false;
   if (w->embedding && w->dec_w_ih && w->dec_w_hh && w->proj_w &&
@@ -548,8 +549,12 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
     if (s16) {
       const int kp = s16_kpad(din);
       HIP_OK(h, launch_split_rows(x, din, (int)rows, din, kp, h->x16.as<uint16_t>(), h->eflag.as<int32_t>(), s));
-      HIP_OK(h, launch_input_proj_s16(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
-                                      h->W + h->L.enc_bias[l], h->gin.as<float>(), s));
+      if (gemm16_waves() == 0)
+        HIP_OK(h, launch_input_proj_s16(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
+                                        h->W + h->L.enc_bias[l], h->gin.as<float>(), s));
+      else
+        HIP_OK(h, launch_input_proj_s16_big(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
+                                            h->W + h->L.enc_bias[l], h->gin.as<float>(), s));
     } else {
       HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
                                   h->gin.as<float>(), s));

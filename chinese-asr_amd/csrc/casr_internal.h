@@ -56,7 +56,7 @@ struct Layout {
   size_t v;                          // [A]
   size_t info;                       // [64]: info[0] = 1 when the s16x3 images are valid
   // s16x3 images (casr_common.h split16) of the MFMA operands, same float count as the f32 ones
-  size_t enc_wih16[CASR_MAX_LAYERS]; // [2*4H][Kp/32][32 hi | 32 lo], Kp = Din rounded up to 32
+  size_t enc_wih16[CASR_MAX_LAYERS]; // [2*4H][Kp/32][32 hi | 32 lo], Kp = Din rounded up to 64
   size_t enc_whh16[CASR_MAX_LAYERS]; // s16 frag-major [2][H/16][4][H/64] (recurrence.hip)
   size_t emb16;                      // [V][E] split words (split16_word)
   size_t dec_w16;                    // s16 frag-major, same tiling / k order as dec_w
@@ -177,9 +177,14 @@ hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, con
 // s16x3 input projection: X16 / W16 are s16 row images with Kp (multiple of 32) k per row
 hipError_t launch_input_proj_s16(const float* X16, int M, int Kp, const float* W16, const float* bias,
                                  float* Gin, hipStream_t s);
+// gemm16.hip: the same product on 256 x 256 tiles (Kp % 64 == 0); gemm16_waves() = 0 selects
+// the 128 x 128 kernel instead
+int gemm16_waves();
+hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
+                                     float* Gin, hipStream_t s);
 hipError_t launch_split_rows(const float* X, int ldx, int M, int K, int Kp, uint16_t* out, int32_t* err,
                              hipStream_t s);
-inline int s16_kpad(int K) { return (K + 31) / 32 * 32; }
+inline int s16_kpad(int K) { return (K + 63) / 64 * 64; }  // even number of 32-k tiles (gemm16.hip)
 hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
                            const float* hprev, float* hnext, float* cst, float* hfin,
                            const int32_t* lens, int B, int Tp, int step, int residual, int row0,

@@ -1,0 +1,191 @@
+// Encoder input projection on the f16 MFMA pipes, 256 x 256 tiles (RNN_RES.forward's
+// nn.LSTM input GEMM, util.py:1258-1275; Gin = x . W_ih^T + b_ih + b_hh for both directions).
+//
+// Why a separate kernel from encoder.hip's 128 x 128 gemm_nt_kernel: s16x3 moves 4 B per operand
+// element (hi + lo halves) but runs the products 16/3 x faster than f32 MFMA, so at 128 x 128
+// the tile is bound by L2 -> LDS bytes (46 B/clk/CU needed against ~30 available,
+// MI355X_MICROARCH.md "2,048 rows shared by every workgroup": 17-19 TB/s chip-wide).  A 256 x 256
+// tile halves the bytes per flop (23 B/clk/CU).
+//
+// Register budget: 4 waves (one per SIMD, 512 registers each), each 128 x 128 = 16 tiles of
+// v_mfma_f32_32x32x16_f16.  Two accumulator sets (hi.hi and cross terms) would need 512
+// accumulator registers, so ONE accumulator holds the whole s16x3 sum scaled by 2^11:
+//     acc = sum_k  a_hi (w_hi 2^11) + a_hi w_lo' + a_lo' w_hi        (x' = (x - x_hi) 2^11)
+//     Gin = acc 2^-11 + bias
+// w_hi 2^11 is formed in registers from the staged w_hi (v_pk_mul_f16 by 2048: exact while
+// |w| < 32, which casr_pack_weights requires before it marks the s16 images valid).  Every
+// product stays exact in f32; the cross terms share the accumulator's rounding, as in the
+// exact-f32 chain.
+//
+// Staging: LDS-DMA (global_load_lds_dwordx4) of 256 rows x 128 B (one 32-k tile of an s16 row
+// image: 32 hi | 32 lo halves) for A and W, two distinct stage buffers of 64 KB, 16-B chunk c of
+// row r at c ^ ((r >> 1) & 7).  Grid: XCD-aware tile order (encoder.hip TileOrder rationale).
+#include <stdlib.h>
+
+#include "casr_common.h"
+#include "casr_internal.h"
+
+namespace casr {
+
+namespace {
+
+constexpr int G16_M = 256, G16_N = 256, G16_K = 32;  // tile rows, columns, k per stage
+constexpr int G16_TILE = G16_M * G16_K;              // 4-B words per operand stage (32 KB)
+
+struct Order16 {
+  int NB, NM, NG;
+  __host__ __device__ int blocks() const { return 8 * (NB / NG) * ((NM + 8 / NG - 1) / (8 / NG)); }
+  __device__ bool tile(int L, int& n, int& m) const {
+    const int x = L & 7, j = L >> 3, nbg = NB / NG;
+    n = (x % NG) * nbg + (j % nbg);
+    m = (j / nbg) * (8 / NG) + (x / NG);
+    return m < NM;
+  }
+};
+
+template <int WN>  // waves along N: 2 -> 4 waves of 128 x 128, 4 -> 8 waves of 128 x 64
+__global__ __launch_bounds__(128 * WN, WN / 2) void gemm16_bias_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
+                                                          const float* __restrict__ bias, float* __restrict__ Cout,
+                                                          int M, int N, int Kp, Order16 order) {
+  __shared__ __attribute__((aligned(16))) float buf0[2 * G16_TILE];  // [A tile | W tile]
+  __shared__ __attribute__((aligned(16))) float buf1[2 * G16_TILE];
+  int nt, mt;
+  if (!order.tile(blockIdx.x, nt, mt)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NT = 8 / WN;                 // 32-column MFMA tiles per wave
+  const int wm = wave / WN, wn = wave % WN;  // wave tile: rows [128 wm, +128) x columns [32 NT wn, +32 NT)
+  const int m0 = mt * G16_M, n0 = nt * G16_N;
+
+  // wave tile 128 x 128 as 4 x 4 tiles of v_mfma_f32_32x32x16_f16 (16 accumulators each):
+  // lane l holds A[row l&31][k = 16s + 8(l>>5) + j] and B[k][col l&31] (j = 0..7) for k-step s,
+  // C/D col = l&31, row = (reg&3) + 8(reg>>2) + 4(l>>5)
+  f32x16 acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const int r32 = lane & 31, hsel = lane >> 5;
+
+  // wave w stages rows [RW w, RW w + RW) of both tiles: RW/8 + RW/8 DMA instructions of 8 rows x 128 B
+  constexpr int RW = 256 / (2 * WN);
+  auto stage = [&](float* dst, int k0) {
+#pragma unroll
+    for (int i = 0; i < RW / 8; ++i) {
+      const int row = wave * RW + i * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+      const int ar = min(m0 + row, M - 1), wr = min(n0 + row, N - 1);
+      float* la = dst + (wave * RW + i * 8) * G16_K;
+      __builtin_amdgcn_global_load_lds(A16 + (size_t)ar * Kp + k0 + c * 4,
+                                       (__attribute__((address_space(3))) void*)la, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(W16 + (size_t)wr * Kp + k0 + c * 4,
+                                       (__attribute__((address_space(3))) void*)(la + G16_TILE), 16, 0, 0);
+    }
+  };
+  const _Float16 two11 = (_Float16)2048.0f;
+  auto compute = [&](const float* src) {
+    const float* as = src;
+    const float* ws = src + G16_TILE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 2 * ks + hsel;  // 16-B chunk of this lane's 8 k (hi); lo is chunk 4 + ch
+      f16x8 wh[NT], wl[NT], w1[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int row = wn * 32 * NT + t * 32 + r32, sw = (row >> 1) & 7;
+        wh[t] = *reinterpret_cast<const f16x8*>(ws + row * G16_K + ((ch ^ sw) << 2));
+        wl[t] = *reinterpret_cast<const f16x8*>(ws + row * G16_K + (((4 + ch) ^ sw) << 2));
+        w1[t] = wh[t] * two11;
+      }
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) {
+        const int row = wm * 128 + tm * 32 + r32, sw = (row >> 1) & 7;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(as + row * G16_K + ((ch ^ sw) << 2));
+        const f16x8 al = *reinterpret_cast<const f16x8*>(as + row * G16_K + (((4 + ch) ^ sw) << 2));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w1[t], acc[tm][t], 0, 0, 0);
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl[t], acc[tm][t], 0, 0, 0);
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh[t], acc[tm][t], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  // Kp % 64 == 0: an even number of k tiles, so the loop body is straight-line (no exit between
+  // the two halves: a branch around a compute block makes hipcc shuffle every accumulator)
+  const int nk = Kp / G16_K;
+  stage(buf0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt += 2) {
+    stage(buf1, (kt + 1) * G16_K);
+    compute(buf0);
+    __syncthreads();  // retires this wave's DMA into buf1 and everyone's reads of buf0
+    if (kt + 2 < nk) stage(buf0, (kt + 2) * G16_K);
+    compute(buf1);
+    __syncthreads();
+  }
+
+  // epilogue: eight 32-row slabs staged through LDS (buf0), stored as whole 1 KB rows
+  constexpr int LDC = G16_N + 4;
+  static_assert(32 * LDC <= 2 * G16_TILE, "slab fits one stage buffer");
+  const int c4 = tid & 63, r0 = tid >> 6;  // 64 float4 per row, 2 WN rows per pass
+  const int col = n0 + c4 * 4;
+  const float4 b4 = col < N ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    // slab p = rows [32p, 32p + 32) = tile tm = p & 3 of the waves with wm = p >> 2
+    if (wm == (p >> 2)) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          buf0[((e & 3) + 8 * (e >> 2) + 4 * hsel) * LDC + wn * 32 * NT + t * 32 + r32] = acc[p & 3][t][e] * S16_LO_INV;
+    }
+    __syncthreads();
+    if (col < N) {
+#pragma unroll
+      for (int row = r0; row < 32; row += 2 * WN) {
+        const int gr = m0 + p * 32 + row;
+        if (gr >= M) break;
+        const float4 v = *reinterpret_cast<const float4*>(buf0 + row * LDC + c4 * 4);
+        *reinterpret_cast<float4*>(Cout + (size_t)gr * N + col) =
+            make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+// CASR_GEMM16_WAVES: 8 (default) or 4 waves per 256 x 256 tile; 0 = encoder.hip's 128 x 128
+// s16 tile (tuning knob)
+int gemm16_waves() {
+  static const int w = [] {
+    const char* e = std::getenv("CASR_GEMM16_WAVES");
+    const int v = e ? std::atoi(e) : 8;
+    return (v == 0 || v == 4) ? v : 8;
+  }();
+  return w;
+}
+
+hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
+                                     float* Gin, hipStream_t s) {
+  const int N = 8 * H;
+  if (Kp % (2 * G16_K) != 0 || M <= 0 || N % G16_N != 0) return hipErrorInvalidValue;
+  const int NB = N / G16_N, NM = (M + G16_M - 1) / G16_M;
+  // smallest group count whose W share (NB/NG slices of 256 rows x Kp words) fits 3/4 of an L2
+  int NG = 1;
+  while (NG < 8 && NB % (NG * 2) == 0 && (size_t)(NB / NG) * G16_N * Kp * 4 > (3u << 20)) NG *= 2;
+  const Order16 order{NB, NM, NG};
+  if (gemm16_waves() == 8)
+    hipLaunchKernelGGL(gemm16_bias_kernel<4>, dim3(order.blocks()), dim3(512), 0, s, X16, W16, bias, Gin, M, N, Kp,
+                       order);
+  else
+    hipLaunchKernelGGL(gemm16_bias_kernel<2>, dim3(order.blocks()), dim3(256), 0, s, X16, W16, bias, Gin, M, N, Kp,
+                       order);
+  return hipGetLastError();
+}
+
+}  // namespace casr

@@ -183,8 +183,9 @@ int casr_set_persistent(casr_handle* h, int enable);
  *   CASR_PREC_S16X3  every f32 operand split as hi + 2^-11 lo (two f16), three f16 MFMAs per
  *                    product (hi.hi + 2^-11 (hi.lo + lo.hi)) on the 16x-faster f16 pipes; 22
  *                    significant operand bits, measured error no larger than the f32 path's.
- * Default S16X3.  A blob whose MFMA weights do not fit the f16 range (|w| >= 2^14 or
- * non-finite) runs F32 whatever is set; casr_get_precision reports the effective mode. */
+ * Default S16X3.  A blob whose MFMA weights do not fit the split (non-finite, |w| >= 2^14, or
+ * an encoder W_ih entry >= 16) runs F32 whatever is set; casr_get_precision reports the
+ * effective mode. */
 enum { CASR_PREC_F32 = 0, CASR_PREC_S16X3 = 1 };
 int casr_set_precision(casr_handle* h, int precision);
 int casr_get_precision(const casr_handle* h); /* effective mode, -1 on a NULL handle */

@@ -71,6 +71,14 @@ def _layout(cfg):
     take("b_attn", A)
     take("w_hidden", HD * A)
     take("v", A)
+    take("info", 64)
+    for l in range(cfg.enc_layers):
+        din = D if l == 0 else C
+        take(f"wih16_{l}", 8 * H * ((din + 63) // 64 * 64))
+        take(f"whh16_{l}", 8 * H * H)
+    take("emb16", cfg.vocab * E)
+    take("dec_w16", 4 * HD * (E + C + HD))
+    take("proj_w16", VP * (C + HD))
     lay["total"] = off
     return lay, VP
 
@@ -125,6 +133,49 @@ def test_packed_layout_contract():
                                   dec["attn_mechanism.W_enc"].T)
     np.testing.assert_array_equal(blob[lay["emb"]:lay["emb"] + CFG.vocab * 256].reshape(CFG.vocab, 256),
                                   dec["embedding.weight"])
+    # s16x3 images: hi = f16_rn(w), lo = f16_rn((w - hi) 2^11); hi + lo 2^-11 within 2^-22 |w|
+    assert blob[lay["info"]] == 1.0
+    h16 = blob.view(np.float16)
+
+    def close(got, want):
+        assert abs(got - float(want)) <= 2.0 ** -21 * abs(float(want)) + 1e-12, (got, want)
+
+    for l in (0, 1):
+        din = 720 if l == 0 else 512
+        kp = (din + 63) // 64 * 64
+        for _ in range(20):
+            n, k = rs.randint(2048), rs.randint(kp)
+            base = 2 * (lay[f"wih16_{l}"] + n * kp) + (k // 32) * 64 + k % 32
+            got = float(h16[base]) + float(h16[base + 32]) / 2048.0
+            want = blob[lay[f"wih{l}"] + n * din + k] if k < din else 0.0
+            close(got, want)
+            if k < din:
+                assert h16[base] == np.float16(want)
+        # recurrent s16 fragments: block (nt, kc) = [j][hi|lo][lane][8], k = 16(lane>>4) + 8j + e
+        for _ in range(20):
+            nt, kc, lane, j, e = rs.randint(64), rs.randint(4), rs.randint(64), rs.randint(2), rs.randint(8)
+            blk = 2 * (lay[f"whh16_{l}"] + (nt * 4 + kc) * 1024)
+            hi = h16[blk + ((j * 2) * 64 + lane) * 8 + e]
+            lo = h16[blk + ((j * 2 + 1) * 64 + lane) * 8 + e]
+            k_local = 16 * (lane >> 4) + 8 * j + e
+            want = _frag(blob, lay[f"whh{l}"], nt, kc, 4, lane & 15, k_local)
+            close(float(hi) + float(lo) / 2048.0, want)
+    e16 = blob[lay["emb16"]:lay["emb16"] + 1000].view(np.float16).astype(np.float64)
+    np.testing.assert_allclose(e16[0::2] + e16[1::2] / 2048.0, blob[lay["emb"]:lay["emb"] + 1000],
+                               rtol=2.0 ** -21, atol=1e-12)
+
+
+def test_out_of_range_weights_fall_back_to_f32_images():
+    """A weight the f16 split cannot carry (|w| >= 16 for the input projection's 2^11-scaled hi)
+    marks the s16 images invalid (blob info word 0): handles then run exact f32 MFMA."""
+    enc, dec = synthetic_state_dicts(CFG)
+    enc = dict(enc)
+    w = enc["rnn.rnn.1.weight_ih_l0"].copy()
+    w[3, 5] = 100.0
+    enc["rnn.rnn.1.weight_ih_l0"] = w
+    blob = L.pack_weights(CFG, enc, dec)
+    lay, _ = _layout(CFG)
+    assert blob[lay["info"]] == 0.0
 
 
 def test_mel_filterbank_matches_reference_fixture():
