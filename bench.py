@@ -24,6 +24,10 @@ import torch  # noqa: E402
 
 METRIC = "utterances/sec + real-time factor, (B,T,F)=(256,800,80) greedy & beam=8"
 PEAK_FP32_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+PEAK_F16_TFLOPS = 2500.0    # MI355X_MICROARCH.md: BF16/F16 MFMA dense peak
+# s16x3 (include/casr.h casr_set_precision): one f32 product = 3 f16 MFMA products, so the
+# f32-equivalent ceiling of the split arithmetic is a third of the f16 peak
+PEAK_S16X3_TFLOPS = PEAK_F16_TFLOPS / 3.0
 PEAK_HBM_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 AUDIO_S_PER_UTT = 8.0       # 800 frames x 10 ms
 
@@ -60,7 +64,8 @@ def kernel_work(cls, B, Tp, R, V, T):
 LAUNCH_UNIT = {
     "rec_step": "rec_layer_kernel: one encoder layer, all Tp steps, both directions, B rows "
                 "(per-step launches rec_step_kernel when the persistent grid does not fit)",
-    "input_proj": "gemm_nt_kernel<StoreBiasEpi>: one layer's input projection, B*Tp rows",
+    "input_proj": "gemm16_bias_kernel (s16x3, 256x256 tiles) or gemm_nt_kernel<StoreBiasEpi> (f32) plus the "
+                  "s16 split of the layer input: one layer's input projection, B*Tp rows",
     "proj": "dgemm_kernel<*,ProjA>: one decode step's vocabulary projection",
     "dec_lstm": "dgemm_kernel<*,DecLstmA>: one decode step's LSTMCell",
     "attention": "attention_kernel: one decode step",
@@ -116,6 +121,10 @@ def main():
     ap.add_argument("--no-beam", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=48)
+    ap.add_argument("--precision", default="s16x3", choices=["s16x3", "f32"],
+                    help="MFMA arithmetic of the timed path (casr_set_precision)")
+    ap.add_argument("--no-f32-compare", action="store_true",
+                    help="skip the side measurement of the exact-f32 MFMA path")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,6 +159,8 @@ def main():
     torch.cuda.synchronize()
     weight_s = time.perf_counter() - t_w
     eng = Engine(cfg, packed=packed, device=dev)
+    eng.set_precision(args.precision)
+    precision = eng.precision()  # effective (f32 if the blob's s16 images are unusable)
 
     B, T = args.batch, args.frames
     fb = torch.from_numpy(fbank_batch(rank * B, B, T)).to(dev)
@@ -200,7 +211,8 @@ def main():
     per_launch_work = work * args.steps / dom_launches
     avg_launch_s = dom_ms / 1000.0 / dom_launches
     if bound == "mfma":
-        achieved, peak, unit = per_launch_work / avg_launch_s / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"
+        peak = PEAK_S16X3_TFLOPS if precision == "s16x3" else PEAK_FP32_TFLOPS
+        achieved, unit = per_launch_work / avg_launch_s / 1e12, "TFLOP/s"
     else:
         achieved, peak, unit = per_launch_work / avg_launch_s / 1e9, PEAK_HBM_GBS, "GB/s"
     # HBM/fabric bytes per launch of the dominant kernel from the committed PMC passes
@@ -232,6 +244,16 @@ def main():
                 "unit": "utt/s", "ms_per_step": 1000.0 * dtb / args.beam_steps,
                 "rtf": dtb / args.beam_steps / (Bb * world * AUDIO_S_PER_UTT)}
 
+    # side measurement: the same greedy step on the exact-f32 MFMA path (not the headline)
+    f32_cmp = None
+    if precision == "s16x3" and not args.no_f32_compare:
+        eng.set_precision("f32")
+        step_greedy()
+        dtf = timed(step_greedy, max(2, args.steps // 2))
+        nf = max(2, args.steps // 2)
+        f32_cmp = {"value": B * world * nf / dtf, "unit": "utt/s", "ms_per_step": 1000.0 * dtf / nf}
+        eng.set_precision(precision)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample, T)
@@ -240,7 +262,11 @@ def main():
         rec = {
             "metric": METRIC, "value": value, "unit": "utt/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32",
+            "vs_baseline": None, "dtype": "f32" if precision == "f32" else "f32/s16x3",
+            "arithmetic": ("f32 data and f32 accumulators; MFMA products " +
+                           ("as s16x3: each f32 operand split into two f16 (hi + 2^-11 lo), 3 f16 MFMAs "
+                            "per product (22 operand bits; measured error below the exact-f32 chain's)"
+                            if precision == "s16x3" else "on exact-f32 v_mfma_f32_16x16x4_f32")),
             "data": "synthetic fbank RandomState(1234+b) (800x80); deterministic synthetic weights "
                     "(SURVEY 8d recipe, proj x40, no EOS bias: all 40 decode steps run)",
             "config": {"workload": f"greedy decode, B={B}/GPU, T={T}, F=80: features + 4-layer BiLSTM "
@@ -253,7 +279,14 @@ def main():
                          "traffic_unit": "bytes per launch (PMC 2 x FETCH_SIZE + WRITE_SIZE)",
                          "algorithmic_bytes": kernel_bytes(dominant, B, Tp, B, cfg.vocab),
                          "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s,
-                         "launch": LAUNCH_UNIT.get(dominant, "one kernel launch")},
+                         "launch": LAUNCH_UNIT.get(dominant, "one kernel launch"),
+                         "peak_basis": ("f16 MFMA dense peak / 3 (s16x3 f32-equivalent)" if bound == "mfma" and
+                                        precision == "s16x3" else "spec peak of the bound"),
+                         **({"latency_bound": True, "per_step_us": 1e6 * avg_launch_s / Tp,
+                             "note": "serial chain of Tp dependent steps per layer; per-step time is "
+                                     "hand-off latency + MFMA + cell (DESIGN.md 3.2)"}
+                            if dominant == "rec_step" else {})},
+            "f32_exact_path": f32_cmp,
             "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},
             "weights_bcast_s": weight_s,
             "device_flags": flags,

@@ -9,9 +9,9 @@
 // ceil(k / KPB) times per step instead of k times.
 //
 // HBM/L2-bound streaming + transcendental work, no MFMA.  512 threads: every phase has
-// 8 waves with several 16 B loads in flight per lane; partial sums are combined through
-// LDS in a fixed order (results are deterministic).  keysT is [B][A][Tq] (Tq = Tp rounded
-// up to 4) so a lane reads 4 consecutive time steps of one key row.
+// 8 waves with all of a lane's 16 B loads of the phase in flight; partial sums are combined
+// through LDS in a fixed order (results are deterministic).  keysT is [B][A][Tq] (Tq = Tp
+// rounded up to 4) so a lane reads 4 consecutive time steps of one key row.
 #include "casr_common.h"
 #include "casr_internal.h"
 
@@ -19,20 +19,20 @@ namespace casr {
 
 constexpr int AT_THREADS = 512;
 constexpr int AT_WAVES = AT_THREADS / 64;
+constexpr int AT_NQ = HD / 16;  // query partials per row (one per 16-unit block of h)
+constexpr int AT_MAXG = 8;      // a-groups of the score phase
 
 __host__ __device__ constexpr int attn_tq(int Tp) { return (Tp + 3) & ~3; }
 
 template <int KPB>
 __host__ __device__ constexpr int attn_scratch_floats(int Tq) {
-  // q partials [16][KPB][A] | score partials [8][KPB][Tq] | context partials [4][KPB][C]
-  return (16 * KPB * A > AT_WAVES * KPB * Tq)
-             ? (16 * KPB * A > 4 * KPB * C ? 16 * KPB * A : 4 * KPB * C)
-             : (AT_WAVES * KPB * Tq > 4 * KPB * C ? AT_WAVES * KPB * Tq : 4 * KPB * C);
+  // score partials [AT_MAXG][KPB][Tq] | context partials [4][KPB][C]
+  return AT_MAXG * KPB * Tq > 4 * KPB * C ? AT_MAXG * KPB * Tq : 4 * KPB * C;
 }
 
 template <int KPB>
 __host__ __device__ constexpr size_t attn_smem_floats(int Tp) {
-  return (size_t)KPB * HD + KPB * A + A + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp);
+  return (size_t)KPB * A + A + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp);
 }
 
 // tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|), on v_exp_f32 / v_rcp_f32.  Absolute
@@ -43,17 +43,21 @@ CASR_DEV float tanh_fast(float x) {
   return copysignf(__fdividef(1.f - e, 1.f + e), x);
 }
 
+// Memory-level parallelism is the design driver: one block (8 waves) per utterance and step
+// streams its keys (A x Tq f32) and values (len x C f32) once per step, so every phase keeps all
+// of a lane's loads of that phase in flight at once (one round trip per phase, not one per
+// unrolled batch).  The query q = h . W_hidden arrives as HD/16 partials written by the decoder
+// LSTM epilogue (decoder.hip DecLstmEpi), so W_hidden is not re-read per block.
 template <int KPB>
 __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
-    float* __restrict__ st, const float* __restrict__ keysT, const float* __restrict__ enc,
-    const int32_t* __restrict__ lens, const float* __restrict__ Wh, const float* __restrict__ vv,
-    int k, int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l, int total) {
+    float* __restrict__ st, const float* __restrict__ qpart, const float* __restrict__ keysT,
+    const float* __restrict__ enc, const int32_t* __restrict__ lens, const float* __restrict__ vv, int R, int k,
+    int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l, int total) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ float wred[2][AT_WAVES][KPB];
   if (done_before(newdone, l) >= total) return;
   const int Tq = attn_tq(Tp);
-  float* hs = sm;                  // [KPB][HD]
-  float* qs = hs + KPB * HD;       // [KPB][A]
+  float* qs = sm;                  // [KPB][A]
   float* vs = qs + KPB * A;        // [A]
   float* xs = vs + A;              // scratch
   float* es = xs + attn_scratch_floats<KPB>(Tq);  // [KPB][Tq]
@@ -63,81 +67,65 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   const int len = min(lens[b], Tp);
   const size_t row0 = (size_t)b * k + j0;
 
-  // 1. h rows and v -> LDS
-  for (int i = tid; i < nk * (HD / 4); i += AT_THREADS) {
-    const int j = i / (HD / 4), c4 = i - j * (HD / 4);
-    reinterpret_cast<float4*>(hs + j * HD)[c4] = reinterpret_cast<const float4*>(st + (row0 + j) * ST + C)[c4];
+  // 1. q = sum of the HD/16 partials (fixed order), v -> LDS
+  for (int i = tid; i < nk * A; i += AT_THREADS) {
+    const int j = i / A, a = i - j * A;
+    const float* qp = qpart + (row0 + j) * A + a;
+    float pv[AT_NQ];
+#pragma unroll
+    for (int p = 0; p < AT_NQ; ++p) pv[p] = qp[(size_t)p * R * A];
+    float q = 0.f;
+#pragma unroll
+    for (int p = 0; p < AT_NQ; ++p) q += pv[p];
+    qs[j * A + a] = q;
   }
   if (tid < A) vs[tid] = vv[tid];
   __syncthreads();
 
-  // 2. q = h . W_hidden: thread = 4 columns x 32 of the 512 rows; 16 partials per column
-  {
-    const int a4 = tid & 31, p = tid >> 5;
-    float acc[KPB][4];
-#pragma unroll
-    for (int j = 0; j < KPB; ++j) acc[j][0] = acc[j][1] = acc[j][2] = acc[j][3] = 0.f;
-    const float* wp = Wh + (size_t)(p * 32) * A + 4 * a4;
-#pragma unroll 8
-    for (int i = 0; i < 32; ++i) {
-      const float4 w4 = *reinterpret_cast<const float4*>(wp + (size_t)i * A);
-#pragma unroll
-      for (int j = 0; j < KPB; ++j) {
-        const float hv = hs[j * HD + p * 32 + i];
-        acc[j][0] = fmaf(hv, w4.x, acc[j][0]);
-        acc[j][1] = fmaf(hv, w4.y, acc[j][1]);
-        acc[j][2] = fmaf(hv, w4.z, acc[j][2]);
-        acc[j][3] = fmaf(hv, w4.w, acc[j][3]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < KPB; ++j)
-      if (j < nk)
-        *reinterpret_cast<float4*>(xs + (p * KPB + j) * A + 4 * a4) =
-            make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
-  }
-  __syncthreads();
-  for (int i = tid; i < nk * A; i += AT_THREADS) {
-    const int j = i / A, a = i - j * A;
-    float q = 0.f;
-#pragma unroll
-    for (int p = 0; p < 16; ++p) q += xs[(p * KPB + j) * A + a];
-    qs[j * A + a] = q;
-  }
-  __syncthreads();
-
-  // 3. scores: wave w owns a in [16w, 16w + 16); lane owns 4 consecutive t
+  // 2. scores.  Thread = (a-group ag, 4-step chunk c): its APG keys rows' float4 at chunk c are
+  // all loaded before use; partial sums per a-group go to LDS and are added in group order.
+  const int nch = Tq / 4;
+  const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
+  const int apg = (A + G - 1) / G;
   const float* kb = keysT + (size_t)b * A * Tq;
-  for (int t0 = 4 * ln; t0 < Tq; t0 += 256) {
+  for (int it = tid; it < G * nch; it += AT_THREADS) {
+    const int ag = it / nch, c = it - ag * nch, t0 = 4 * c;
+    const int a0 = ag * apg, a1 = min(A, a0 + apg);
     float e4[KPB][4];
 #pragma unroll
     for (int j = 0; j < KPB; ++j) e4[j][0] = e4[j][1] = e4[j][2] = e4[j][3] = 0.f;
     if (t0 < len) {
-#pragma unroll 4
-      for (int ai = 0; ai < A / AT_WAVES; ++ai) {
-        const int a = wv * (A / AT_WAVES) + ai;
-        const float4 kv = *reinterpret_cast<const float4*>(kb + (size_t)a * Tq + t0);
-        const float va = vs[a];
+      constexpr int CH = 20;  // keys rows in flight per batch (apg = 19 at Tp = 266)
+      for (int ab = a0; ab < a1; ab += CH) {
+        float4 kv[CH];
 #pragma unroll
-        for (int j = 0; j < KPB; ++j)
-          if (j < nk) {
-            const float qa = qs[j * A + a];
-            e4[j][0] = __fadd_rn(e4[j][0], __fmul_rn(tanh_fast(kv.x + qa), va));
-            e4[j][1] = __fadd_rn(e4[j][1], __fmul_rn(tanh_fast(kv.y + qa), va));
-            e4[j][2] = __fadd_rn(e4[j][2], __fmul_rn(tanh_fast(kv.z + qa), va));
-            e4[j][3] = __fadd_rn(e4[j][3], __fmul_rn(tanh_fast(kv.w + qa), va));
-          }
+        for (int i = 0; i < CH; ++i)
+          kv[i] = ab + i < a1 ? *reinterpret_cast<const float4*>(kb + (size_t)(ab + i) * Tq + t0)
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          if (ab + i >= a1) break;
+          const float va = vs[ab + i];
+#pragma unroll
+          for (int j = 0; j < KPB; ++j)
+            if (j < nk) {
+              const float qa = qs[j * A + ab + i];
+              e4[j][0] = __fadd_rn(e4[j][0], __fmul_rn(tanh_fast(kv[i].x + qa), va));
+              e4[j][1] = __fadd_rn(e4[j][1], __fmul_rn(tanh_fast(kv[i].y + qa), va));
+              e4[j][2] = __fadd_rn(e4[j][2], __fmul_rn(tanh_fast(kv[i].z + qa), va));
+              e4[j][3] = __fadd_rn(e4[j][3], __fmul_rn(tanh_fast(kv[i].w + qa), va));
+            }
+        }
       }
     }
 #pragma unroll
     for (int j = 0; j < KPB; ++j)
       if (j < nk)
-        *reinterpret_cast<float4*>(xs + (wv * KPB + j) * Tq + t0) =
-            make_float4(e4[j][0], e4[j][1], e4[j][2], e4[j][3]);
+        *reinterpret_cast<float4*>(xs + (ag * KPB + j) * Tq + t0) = make_float4(e4[j][0], e4[j][1], e4[j][2], e4[j][3]);
   }
   __syncthreads();
 
-  // combine the 8 wave partials (fixed order), mask past len, row maxima
+  // combine the G group partials (fixed order), mask past len, row maxima
   float lmax[KPB];
 #pragma unroll
   for (int j = 0; j < KPB; ++j) {
@@ -147,8 +135,9 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
         float ev = -INFINITY;
         if (t < len) {
           const float* x = xs + j * Tq + t;
-          const int ws = KPB * Tq;
-          ev = ((x[0] + x[ws]) + (x[2 * ws] + x[3 * ws])) + ((x[4 * ws] + x[5 * ws]) + (x[6 * ws] + x[7 * ws]));
+          const int gs = KPB * Tq;
+          ev = x[0];
+          for (int gg = 1; gg < G; ++gg) ev += x[gg * gs];
         }
         es[j * Tq + t] = ev;
         lmax[j] = fmaxf(lmax[j], ev);
@@ -171,7 +160,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     rmax[j] = m;
     lsum[j] = 0.f;
   }
-  // 4. softmax over t (torch: exp(x - max), sum, then * 1/sum)
+  // 3. softmax over t (torch: exp(x - max), sum, then * 1/sum)
 #pragma unroll
   for (int j = 0; j < KPB; ++j)
     if (j < nk)
@@ -196,36 +185,47 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
           ((wred[1][4][j] + wred[1][5][j]) + (wred[1][6][j] + wred[1][7][j]));
     rinv[j] = 1.0f / s;
   }
-  const size_t R = (size_t)gridDim.x * k;
+  const size_t RR = (size_t)R;
 #pragma unroll
   for (int j = 0; j < KPB; ++j)
     if (j < nk)
       for (int t = tid; t < Tq; t += AT_THREADS) {
         const float al = es[j * Tq + t] * rinv[j];
         es[j * Tq + t] = al;
-        if (align && t < Tp) align[(size_t)t * R + row0 + j] = al;
+        if (align && t < Tp) align[(size_t)t * RR + row0 + j] = al;
       }
   __syncthreads();
 
-  // 5. context: thread = 4 columns x every 4th t (4 partials, combined in a fixed order)
+  // 4. context: thread = 4 columns x every 4th t (4 partials, combined in a fixed order); 32
+  // value rows in flight per lane
   {
     const int c4 = tid & 127, tp = tid >> 7;
     float acc[KPB][4];
 #pragma unroll
     for (int j = 0; j < KPB; ++j) acc[j][0] = acc[j][1] = acc[j][2] = acc[j][3] = 0.f;
     const float* eb = enc + (size_t)b * Tp * C + 4 * c4;
-#pragma unroll 8
-    for (int t = tp; t < len; t += 4) {
-      const float4 v4 = *reinterpret_cast<const float4*>(eb + (size_t)t * C);
+    constexpr int CT = 32;
+    for (int tb = tp; tb < len; tb += 4 * CT) {
+      float4 v4[CT];
 #pragma unroll
-      for (int j = 0; j < KPB; ++j)
-        if (j < nk) {
-          const float al = es[j * Tq + t];
-          acc[j][0] = __fadd_rn(acc[j][0], __fmul_rn(al, v4.x));
-          acc[j][1] = __fadd_rn(acc[j][1], __fmul_rn(al, v4.y));
-          acc[j][2] = __fadd_rn(acc[j][2], __fmul_rn(al, v4.z));
-          acc[j][3] = __fadd_rn(acc[j][3], __fmul_rn(al, v4.w));
-        }
+      for (int i = 0; i < CT; ++i) {
+        const int t = tb + 4 * i;
+        v4[i] = t < len ? *reinterpret_cast<const float4*>(eb + (size_t)t * C) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < CT; ++i) {
+        const int t = tb + 4 * i;
+        if (t >= len) break;
+#pragma unroll
+        for (int j = 0; j < KPB; ++j)
+          if (j < nk) {
+            const float al = es[j * Tq + t];
+            acc[j][0] = __fadd_rn(acc[j][0], __fmul_rn(al, v4[i].x));
+            acc[j][1] = __fadd_rn(acc[j][1], __fmul_rn(al, v4[i].y));
+            acc[j][2] = __fadd_rn(acc[j][2], __fmul_rn(al, v4[i].z));
+            acc[j][3] = __fadd_rn(acc[j][3], __fmul_rn(al, v4[i].w));
+          }
+      }
     }
 #pragma unroll
     for (int j = 0; j < KPB; ++j)
@@ -250,8 +250,8 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 }
 
 template <int KPB>
-static hipError_t launch_kpb(const DecodeArgs& a, float* st, float* align, int32_t* newdone, int l,
-                             int total, hipStream_t s) {
+static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart, float* align, int32_t* newdone,
+                             int l, int total, hipStream_t s) {
   const size_t shm = attn_smem_floats<KPB>(a.Tp) * sizeof(float);
   static size_t raised = 0;  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950)
   if (shm > raised) {
@@ -261,16 +261,16 @@ static hipError_t launch_kpb(const DecodeArgs& a, float* st, float* align, int32
     raised = shm;
   }
   dim3 grid(a.B, (a.k + KPB - 1) / KPB);
-  hipLaunchKernelGGL(attention_kernel<KPB>, grid, dim3(AT_THREADS), shm, s, st, a.keysT, a.enc, a.lens,
-                     a.W + a.L.w_hidden, a.W + a.L.v, a.k, a.Tp, align, newdone, l, total);
+  hipLaunchKernelGGL(attention_kernel<KPB>, grid, dim3(AT_THREADS), shm, s, st, qpart, a.keysT, a.enc, a.lens,
+                     a.W + a.L.v, a.B * a.k, a.k, a.Tp, align, newdone, l, total);
   return hipGetLastError();
 }
 
-hipError_t launch_attention_step(const DecodeArgs& a, float* st, float* align, int32_t* newdone,
-                                 int l, int total, hipStream_t s) {
-  if (a.k == 1) return launch_kpb<1>(a, st, align, newdone, l, total, s);
-  if (a.k == 2) return launch_kpb<2>(a, st, align, newdone, l, total, s);
-  return launch_kpb<4>(a, st, align, newdone, l, total, s);
+hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
+                                 int32_t* newdone, int l, int total, hipStream_t s) {
+  if (a.k == 1) return launch_kpb<1>(a, st, qpart, align, newdone, l, total, s);
+  if (a.k == 2) return launch_kpb<2>(a, st, qpart, align, newdone, l, total, s);
+  return launch_kpb<4>(a, st, qpart, align, newdone, l, total, s);
 }
 
 size_t attention_smem_bytes(int k, int Tp) {

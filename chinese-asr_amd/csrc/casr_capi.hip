@@ -688,7 +688,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   const size_t smem = attention_smem_bytes(k, Tp);
   if (smem > 160 * 1024)
     return fail(h, CASR_ERR_UNSUPPORTED, "attention needs %zu B of LDS (k=%d, Tp=%d) > 160 KiB", smem, k, Tp);
-  HIP_OK(h, h->st.ensure((size_t)2 * R * ST * sizeof(float)));
+  HIP_OK(h, h->st.ensure(((size_t)2 * R * ST + (size_t)(HD / 16) * R * A) * sizeof(float)));
   HIP_OK(h, h->logits.ensure((size_t)R * V * sizeof(float)));
   HIP_OK(h, h->small.ensure((size_t)(6 * R + L + B + R + 1) * sizeof(int32_t) + 256));
   HIP_OK(h, h->bp.ensure((size_t)L * R * sizeof(int32_t)));
@@ -697,6 +697,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   DecodeBufs& d = h->d;
   d.st[0] = h->st.as<float>();
   d.st[1] = d.st[0] + (size_t)R * ST;
+  d.qpart = d.st[1] + (size_t)R * ST;
   d.logits = h->logits.as<float>();
   int32_t* sp = h->small.as<int32_t>();
   d.tok[0] = sp;

@@ -100,6 +100,19 @@ CASR_DEV float wave_sum(float v) {
   return v;
 }
 
+// Hardware-exp forms (v_exp_f32 / v_rcp_f32): relative error ~|x| 1e-7 for the sigmoid, absolute
+// error ~1e-7 for tanh (diagnostic variant of the cell, CASR_REC_FASTCELL)
+CASR_DEV float sigmoid_hw(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+CASR_DEV float tanh_hw(float x) {
+  const float e = __expf(-2.f * fabsf(x));
+  return copysignf(__fdividef(1.f - e, 1.f + e), x);
+}
+CASR_DEV void lstm_cell_hw(float gi, float gf, float gg, float go, float c, float& h2, float& c2) {
+  const float i = sigmoid_hw(gi), f = sigmoid_hw(gf), g = tanh_hw(gg), o = sigmoid_hw(go);
+  c2 = __fadd_rn(__fmul_rn(f, c), __fmul_rn(i, g));
+  h2 = __fmul_rn(o, tanh_hw(c2));
+}
+
 // LSTM cell with PyTorch gate order (i, f, g, o): c' = f*c + i*g, h' = o*tanh(c').
 CASR_DEV void lstm_cell(float gi, float gf, float gg, float go, float c, float& h2, float& c2) {
   const float i = sigmoid_acc(gi);

@@ -205,6 +205,7 @@ hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, cons
 struct DecodeBufs {
   float* st[2];          // [R][ST]
   float* logits;         // [R][V]
+  float* qpart;          // [HD/16][R][A] attention query partials, one per 16-unit block of h
   int32_t* tok[2];       // [R]
   int32_t* src[2];       // [R]
   float* score[2];       // [R]
@@ -236,8 +237,8 @@ struct DecodeArgs {
 };
 
 // attention.hip: one decode step's additive attention for all R rows (writes ctx into st)
-hipError_t launch_attention_step(const DecodeArgs& a, float* st, float* align, int32_t* newdone,
-                                 int l, int total, hipStream_t s);
+hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
+                                 int32_t* newdone, int l, int total, hipStream_t s);
 size_t attention_smem_bytes(int k, int Tp);
 
 hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, 
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) acc[tn] += part[((j * WR + ws) * 4 + tn) * 64 + lane];
   // lane holds rows rb*BM + ws*16 + 4g + e (e = 0..3), column nb*64 + tn*16 + r
-  epi.run(acc, rb * BM + ws * 16 + 4 * g, nb, r);
+  epi.template run<4>(acc, rb * BM + ws * 16 + 4 * g, nb, r);
 }
 
 // 64-row blocks where that still gives >= 2 blocks per CU, else 32-row blocks
@@ -236,29 +236,57 @@ struct DecLstmA {
 
 // LSTMCell epilogue: the 4 n-tiles of a 64-column block are the 4 gates of 16 hidden units
 // (gate-interleaved packing), so each lane holds all four gates of its (row, unit) cells.
+// It also starts the attention query (attention.py:92, q = h . W_hidden): the wave's 16 x 16
+// tile of h (16 rows x this block's 16 units) times W_hidden[16 units][A] is one partial of q,
+// written to qpart[nb][row] (the attention kernel adds the HD/16 partials in a fixed order).
+// The tile is transposed through LDS into the A operand of 32 exact-f32 MFMAs (16x16x4).
 struct DecLstmEpi {
   const float* bias;  // packed [4HD]
   const float* st_old;
   float* st_new;
   DecLstmA rows;      // guarded predecessor lookup
   const int32_t* newdone;
+  const float* w_hidden;  // [HD][A]
+  float* qpart;           // [HD/16][R][A]
   int R, l, total;
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
-  __device__ __forceinline__ void run(const f32x4 (&acc)[4], int row0, int nb, int u) const {
+  template <int NTN = 4>
+  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u) const {
+    static_assert(NTN == 4, "the LSTM cell needs the 4 gate tiles of a 64-column block");
+    __shared__ float ht[4][16][17];  // per row-slab wave: h tile [row][unit]
+    const int lane = threadIdx.x & 63, ws = (row0 >> 4) & 3, g = lane >> 4;
     const int U = nb * 16 + u;
     float bg[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) bg[g] = bias[nb * 64 + g * 16 + u];
+    for (int gt = 0; gt < 4; ++gt) bg[gt] = bias[nb * 64 + gt * 16 + u];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int row = row0 + e;
-      if (row >= R) break;
-      float h2, c2;
-      lstm_cell(acc[0][e] + bg[0], acc[1][e] + bg[1], acc[2][e] + bg[2], acc[3][e] + bg[3],
-                st_old[(size_t)rows.safe_src(row) * ST + C + HD + U], h2, c2);
-      st_new[(size_t)row * ST + C + U] = h2;
-      st_new[(size_t)row * ST + C + HD + U] = c2;
-      reinterpret_cast<uint32_t*>(st_new)[(size_t)row * ST + ST16 + C + U] = split16_word(h2);
+      float h2 = 0.f, c2;
+      if (row < R) {
+        lstm_cell(acc[0][e] + bg[0], acc[1][e] + bg[1], acc[2][e] + bg[2], acc[3][e] + bg[3],
+                  st_old[(size_t)rows.safe_src(row) * ST + C + HD + U], h2, c2);
+        st_new[(size_t)row * ST + C + U] = h2;
+        st_new[(size_t)row * ST + C + HD + U] = c2;
+        reinterpret_cast<uint32_t*>(st_new)[(size_t)row * ST + ST16 + C + U] = split16_word(h2);
+      }
+      ht[ws][4 * g + e][u] = h2;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read back by other lanes of this wave
+    __builtin_amdgcn_wave_barrier();
+    const int rbase = row0 - 4 * g;  // first row of this wave's slab
+    const float* wp = w_hidden + (size_t)(nb * 16 + g) * A + (lane & 15);
+#pragma unroll
+    for (int at = 0; at < A / 16; ++at) {
+      f32x4 q = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        q = mfma16x16x4(ht[ws][lane & 15][4 * kk + g], wp[(size_t)(4 * kk) * A + at * 16], q);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = rbase + 4 * g + e;
+        if (row < R) qpart[((size_t)nb * R + row) * A + at * 16 + (lane & 15)] = q[e];
+      }
     }
   }
 };
@@ -278,10 +306,11 @@ struct ProjEpi {
   const int32_t* newdone;
   int R, V, l, total;
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
-  __device__ __forceinline__ void run(const f32x4 (&acc)[4], int row0, int nb, int u) const {
+  template <int NTN = 4>
+  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u) const {
 #pragma unroll
-    for (int tn = 0; tn < 4; ++tn) {
-      const int n = nb * 64 + tn * 16 + u;
+    for (int tn = 0; tn < NTN; ++tn) {
+      const int n = (nb * NTN + tn) * 16 + u;
       if (n >= V) continue;
       const float bn = bias[n];
 #pragma unroll
@@ -726,13 +755,13 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   {
     ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
     DecLstmA asrc{a.W + (a.s16 ? a.L.emb16 : a.L.emb), st_old, d.tok[l & 1], d.src[l & 1], d.err, R, a.V, a.s16};
-    DecLstmEpi epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, R, l, total};
+    DecLstmEpi epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, a.W + a.L.w_hidden, d.qpart, R, l, total};
     launch_dgemm(HD / 16, R, KDEC / DG_BK, a.W + (a.s16 ? a.L.dec_w16 : a.L.dec_w), asrc, epi, a.s16, s);
   }
   hipError_t e;
   {
     ProfScope ps(a.prof, CASR_K_ATTENTION, s);
-    e = launch_attention_step(a, st_new, align, d.newdone, l, total, s);
+    e = launch_attention_step(a, st_new, d.qpart, align, d.newdone, l, total, s);
   }
   if (e != hipSuccess) return e;
   {

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
-    int32_t* __restrict__ err, uint32_t* __restrict__ trace) {
+    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int fastcell) {
   constexpr int NW = RG / 4;           // waves: 4 k-chunks x RG/16 row halves
   __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
@@ -228,7 +228,10 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
         gate[tn] = sum + gin_v[tn];
       }
       float c2;
-      lstm_cell(gate[0], gate[1], gate[2], gate[3], c, h2, c2);
+      if (fastcell)
+        lstm_cell_hw(gate[0], gate[1], gate[2], gate[3], c, h2, c2);
+      else
+        lstm_cell(gate[0], gate[1], gate[2], gate[3], c, h2, c2);
       c = c2;
       const int t = (d == 0) ? s : (len - 1 - s);
       const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
@@ -294,8 +297,12 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
   const int RG = rec_rg();
   dim3 grid(H / 16, (B + RG - 1) / RG, 2);
   auto go = [&](auto kern, int threads) {
+    static const int fastcell = [] {
+      const char* e = std::getenv("CASR_REC_FASTCELL");
+      return e && std::atoi(e) == 1 ? 1 : 0;
+    }();
     hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens, B, Bp, Tp,
-                       residual, err, trace);
+                       residual, err, trace, fastcell);
   };
   if (RG == 16)
     s16 ? go(rec_layer_kernel<16, true>, 256) : go(rec_layer_kernel<16, false>, 256);
