@@ -522,6 +522,8 @@ __device__ __forceinline__ void wave_merge(TopList<K2>& L, int n, float* outv, i
 // per-lane sorted list), the lane lists merged with wave shuffles to the row's top-2k, then
 // wave 0 merges the k rows' lists from LDS into the utterance's top-2k (torch.topk over
 // the k*V flattened scores, model.py:860-865; ties -> lower flat index).
+constexpr int BS_CAP = 256;  // threshold candidates kept per row (beyond: full selection)
+
 template <int K2>
 __global__ __launch_bounds__(512) void beam_select_kernel(
     const float* __restrict__ logits, int V, int B, int k, int l, int L, int eos, float temperature,
@@ -534,6 +536,9 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
   __shared__ int ri_s[KMAX_BEAM][K2];
   __shared__ float cv[K2];
   __shared__ int ci[K2];
+  __shared__ float cv_s[8][BS_CAP];  // per-wave threshold candidates
+  __shared__ int ci_s[8][BS_CAP];
+  __shared__ int cnt_s[8];
   if (done_before(newdone, l) >= B) return;
   const int b = blockIdx.x, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
   const int R = B * k;
@@ -544,18 +549,18 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
   for (int j = wv; j < nrows; j += 8) {
     const float* x = logits + (size_t)(b * k + j) * V;
     const float4* x4 = reinterpret_cast<const float4*>(x);
-    float m = -INFINITY;
+    float lm = -INFINITY;  // this lane's largest x / T
     if (vec) {
 #pragma unroll 4
       for (int i = ln; i < V / 4; i += 64) {
         const float4 q = x4[i];
-        m = fmaxf(m, fmaxf(fmaxf(q.x / temperature, q.y / temperature),
-                           fmaxf(q.z / temperature, q.w / temperature)));
+        lm = fmaxf(lm, fmaxf(fmaxf(q.x / temperature, q.y / temperature),
+                             fmaxf(q.z / temperature, q.w / temperature)));
       }
     } else {
-      for (int v = ln; v < V; v += 64) m = fmaxf(m, x[v] / temperature);
+      for (int v = ln; v < V; v += 64) lm = fmaxf(lm, x[v] / temperature);
     }
-    m = wave_max(m);
+    const float m = wave_max(lm);
     float s = 0.f;
     if (vec) {
 #pragma unroll 4
@@ -570,10 +575,49 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     s = wave_sum(s);
     const float lse = logf(s) + m;
     const float sc = score_cur[b * k + j];
-    TopList<K2> tl;
-    tl.init();
+    // Threshold filter for the row's top-2k (model.py:834-865 ranks val = (x/T - lse) + score):
+    // val is monotone in x, so a lane's largest val is (lm - lse) + sc, and the 2k-th largest of
+    // the 64 lane maxima, tau, bounds the row's 2k-th best val from below (those 2k maxima are
+    // distinct elements).  Only elements with val >= tau (typically a few dozen) enter the
+    // sorted-list selection, instead of every element in every lane (divergent insertions).
+    float lt = (lm - lse) + sc, tau = -INFINITY;
+    for (int c = 0; c < n2k; ++c) {
+      const float mx = wave_max(lt);
+      tau = mx;
+      const unsigned long long hit = __ballot(lt == mx);
+      if (hit && ln == __ffsll((long long)hit) - 1) lt = -INFINITY;
+    }
+    if (ln == 0) cnt_s[wv] = 0;
+    __builtin_amdgcn_wave_barrier();
+    auto offer = [&](float val, int idx) {
+      if (val >= tau) {
+        const int slot = atomicAdd(&cnt_s[wv], 1);
+        if (slot < BS_CAP) {
+          cv_s[wv][slot] = val;
+          ci_s[wv][slot] = idx;
+        }
+      }
+    };
     if (vec) {
 #pragma unroll 2
+      for (int i = ln; i < V / 4; i += 64) {
+        const float4 q = x4[i];
+        offer((q.x / temperature - lse) + sc, j * V + 4 * i);
+        offer((q.y / temperature - lse) + sc, j * V + 4 * i + 1);
+        offer((q.z / temperature - lse) + sc, j * V + 4 * i + 2);
+        offer((q.w / temperature - lse) + sc, j * V + 4 * i + 3);
+      }
+    } else {
+      for (int v = ln; v < V; v += 64) offer((x[v] / temperature - lse) + sc, j * V + v);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int nc = cnt_s[wv];
+    TopList<K2> tl;
+    tl.init();
+    if (nc <= BS_CAP) {
+      for (int p = ln; p < nc; p += 64) tl.insert(cv_s[wv][p], ci_s[wv][p]);
+    } else if (vec) {  // more ties at tau than the buffer holds: every element
       for (int i = ln; i < V / 4; i += 64) {
         const float4 q = x4[i];
         tl.insert((q.x / temperature - lse) + sc, j * V + 4 * i);  // model.py:834-836
