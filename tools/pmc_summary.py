@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 CLASS_OF = {  # bench.py kernel classes -> kernel-name prefixes (after short())
-    "input_proj": "gemm_nt_kernel<StoreBiasEpi>",
+    "input_proj": "gemm16_bias_kernel",
     "keys": "gemm_nt_kernel<KeysEpi>",
     "rec_step": "rec_layer_kernel",
     "dec_lstm": "dgemm_kernel<2, DecLstmA",
