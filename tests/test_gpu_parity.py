@@ -33,6 +33,7 @@ def eng(request):
     from casr.engine import Engine
     e = Engine(CFG, *synthetic_state_dicts(CFG, peaked=False))
     e.set_precision(request.param)
+    e.requested = request.param
     assert e.precision() == request.param
     yield e
     e.close()
@@ -283,3 +284,34 @@ def test_batch_invariance_and_determinism(eng):
     eng.encode(feat[:16].contiguous(), flen[:16].contiguous())
     t2 = eng.beam(8)["tokens"].cpu()
     assert torch.equal(t1[:16], t2)
+
+
+def test_out_of_range_weights_run_f32(eng):
+    """A blob whose weights the f16 split cannot carry (an encoder W_ih entry >= 16) is marked
+    invalid at pack time; a handle bound to it reports and runs exact f32 whatever is requested,
+    and still decodes like the CPU oracle on the same weights."""
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
+    enc_sd = dict(enc_sd)
+    w = enc_sd["rnn.rnn.0.weight_ih_l0"].copy()
+    w[7, 11] = 20.0
+    enc_sd["rnn.rnn.0.weight_ih_l0"] = w
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    assert eng.precision() == "f32"
+    frames = [150, 96]
+    fbs = [fbank_for(b, t) for b, t in enumerate(frames)]
+    x = np.zeros((2, max(frames), 80), np.float32)
+    for b, f in enumerate(fbs):
+        x[b, :len(f)] = f
+    feat, flen = eng.features(torch.from_numpy(x).to(eng.device), torch.tensor(frames, dtype=torch.int32,
+                                                                               device=eng.device))
+    eng.encode(feat, flen)
+    out = eng.greedy()
+    assert eng.device_flags() == 0
+    toks, _ = greedy_outputs(out["tokens"].cpu().numpy(), out["out_len"].cpu().numpy(),
+                             out["finished"].cpu().numpy().astype(bool), out["accum"].cpu().numpy())
+    feats = [O.features_from_fbank(f) for f in fbs]
+    ref = O.greedy_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd)
+    assert toks == ref["tokens"]
+    # a valid blob restores the requested arithmetic
+    eng.bind(pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True)))
+    assert eng.precision() == eng.requested
