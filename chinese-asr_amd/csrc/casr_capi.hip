@@ -589,7 +589,7 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
         HIP_OK(h, hipStreamSynchronize(s));
         tbuf.release();
         if (FILE* f = std::fopen(trace_path, "wb")) {
-          const int32_t hdr[4] = {rec_layer_grid_blocks(B), rec_layer_waves(), Tp, 5};
+          const int32_t hdr[5] = {rec_layer_grid_blocks(B), rec_layer_waves(), Tp, 5, rec_layer_producers()};
           std::fwrite(hdr, sizeof hdr, 1, f);
           std::fwrite(hostv.data(), 4, hostv.size(), f);
           std::fclose(f);

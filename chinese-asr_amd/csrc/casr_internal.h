@@ -193,6 +193,7 @@ hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xi
 size_t rec_layer_granule_bytes(int B);
 int rec_layer_grid_blocks(int B);
 int rec_layer_waves();  // waves per workgroup (trace layout)
+int rec_layer_producers();  // workgroups per row group (trace layout)
 hipError_t rec_layer_occupancy(int* blocks_per_cu);
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s);  // before EVERY launch_rec_layer
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,

@@ -32,6 +32,7 @@
 // s_memrealtime and a pass count); a timeout sets CASR_DEV_REC_TIMEOUT and the workgroup leaves
 // the loop.
 #include <stdlib.h>
+#include <string.h>
 
 #include "casr_common.h"
 #include "casr_internal.h"
@@ -68,30 +69,48 @@ CASR_DEV float decode_granule(uint32_t x) {
   return (x & 0x7FFFFFFFu) == NONFINITE ? __uint_as_float(0x7FC00000u) : __uint_as_float(x);
 }
 
-// RG batch rows per workgroup (32: 8 waves, one workgroup per CU; 16: 4 waves, two per CU)
+// Workgroup = RG batch rows x UW hidden units (x 4 gates) of one direction; NW = 4 k-chunks x
+// RG/16 row halves x UW/16 unit halves waves.  32 x 16 (default): 16 producers per row group;
+// 16 x 32: 8 producers per row group (a consumer waits on fewer workgroups; the two unit-half
+// waves of a k-chunk sweep the same words); 16 x 16: 4 waves, two workgroups per CU.
 // S16: W_hh is the s16 fragment image (casr_capi.hip pack_frag16) and the contraction runs as
 // s16x3 on v_mfma_f32_16x16x32_f16 (2 k-steps of 32 per 64-unit chunk, 24 MFMAs per wave and
 // step instead of 64 f32 ones at twice the cycles each).  Lane (r, g) of k-step j covers units
 // 16g + 8j + e of its chunk: exactly the granule words its sweep already loaded.
-template <int RG, bool S16>
-__global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
+template <int RG, int UW, bool S16>
+__global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
-    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int fastcell) {
-  constexpr int NW = RG / 4;           // waves: 4 k-chunks x RG/16 row halves
+    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int fastcell, int nrg) {
+  constexpr int NW = RG * UW / 64;      // waves: 4 k-chunks x RG/16 row halves x UW/16 unit halves
   __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
-  const int ub = blockIdx.x, rg = blockIdx.y, d = blockIdx.z;
+  // ---- placement (speed only, never correctness).  Workgroups are dealt round-robin over the 8
+  // XCDs (MI355X_MICROARCH.md "Workgroup dispatch"), so ids L and L + 8 share one: the P members
+  // of a hand-off group (the unit blocks of one row group and direction) take ids with equal L % 8
+  // and exchange h inside one XCD.  Measured: 3.49 -> 3.07 us per step.
+  constexpr int P = H / UW;  // producers per group
+  const int G = 2 * nrg, L = blockIdx.x;
+  int grp, mem;
+  if (G % 8 == 0) {
+    const int x = L & 7, j = L >> 3;
+    grp = x * (G / 8) + j / P;
+    mem = j % P;
+  } else {
+    grp = L / P;
+    mem = L % P;
+  }
+  const int ub = mem, rg = grp % nrg, d = grp / nrg;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int kc = w & 3, half = w >> 2;
+  const int kc = w & 3, half = (w >> 2) % (RG / 16), uh = (w >> 2) / (RG / 16);
   const size_t plane = (size_t)Bp * H;  // granules per direction per buffer
 
-  // ---- epilogue cell of this thread: batch row rl (of 32), unit u (of 16)
-  const int rl = tid >> 4, u = tid & 15;
+  // ---- epilogue cell of this thread: batch row rl (of RG), unit u (of UW)
+  const int rl = tid / UW, u = tid % UW;
   const int b = rg * RG + rl;
   const int len = b < B ? min(max(lens[b], 0), Tp) : 0;
-  const int U = ub * 16 + u;
+  const int U = ub * UW + u;
   const size_t si = ((size_t)d * B + b) * H + U;       // hfin / cst index (valid when b < B)
   const size_t gi = ((size_t)d * Bp + b) * H + U;      // granule index within a buffer
   if (tid == 0) {
@@ -106,7 +125,7 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
   float4 bw[4][4];
 #pragma unroll
   for (int tn = 0; tn < 4; ++tn) {
-    const float* wb = Wd + ((size_t)(ub * 4 + tn) * NKC + kc) * FRAG + lane * 4;
+    const float* wb = Wd + ((size_t)((ub * (UW / 16) + uh) * 4 + tn) * NKC + kc) * FRAG + lane * 4;
 #pragma unroll
     for (int q = 0; q < 4; ++q) bw[tn][q] = *reinterpret_cast<const float4*>(wb + q * 256);
   }
@@ -126,14 +145,14 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
   auto load_operands = [&](int s, float (&g)[4], float& xr) {
     if (s < len) {
       const int t = (d == 0) ? s : (len - 1 - s);
-      const float* gp = Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + ub * 64;
+      const float* gp = Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + (U >> 4) * 64;
 #pragma unroll
-      for (int tn = 0; tn < 4; ++tn) g[tn] = gp[tn * 16 + u];
+      for (int tn = 0; tn < 4; ++tn) g[tn] = gp[tn * 16 + (U & 15)];
       if (residual) xr = xin[((size_t)b * Tp + t) * C + d * H + U];
     }
   };
   load_operands(0, gin_v, x_res);
-  uint32_t* tr = trace ? trace + ((size_t)((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * NW + w) * Tp * 5 : nullptr;
+  uint32_t* tr = trace ? trace + ((size_t)(grp * P + mem) * NW + w) * Tp * 5 : nullptr;
   for (int s = 0; s < tmax; ++s) {
     const bool act = s < len;
     uint32_t npass = 0;
@@ -215,8 +234,8 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
     if (tr && lane == 0) tr[s * 5 + 2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 
     // cell (same reduction order as rec_step_kernel: k-chunks 0..3, then + Gin)
-    const int hw = (rl >> 4) * 4, rr = rl & 15;
-    const int src_lane = u + 16 * (rr >> 2), reg = rr & 3;
+    const int hw = ((rl >> 4) + (RG / 16) * (u >> 4)) * 4, rr = rl & 15;
+    const int src_lane = (u & 15) + 16 * (rr >> 2), reg = rr & 3;
     float h2 = 0.f;
     if (act) {
       float gate[4];
@@ -252,34 +271,46 @@ __global__ __launch_bounds__(RG * 16, 2) void rec_layer_kernel(
 
 }  // namespace
 
-static int rec_rg() {  // CASR_REC_RG=16 selects 16-row workgroups (diagnostics / tuning)
-  static const int rg = [] {
-    const char* e = std::getenv("CASR_REC_RG");
-    return (e && std::atoi(e) == 16) ? 16 : 32;
+// CASR_REC_LAYOUT = rows x units per workgroup: 32x16 (default), 16x32 or 16x16 (tuning knob)
+static int rec_layout() {
+  static const int v = [] {
+    const char* e = std::getenv("CASR_REC_LAYOUT");
+    if (e && strcmp(e, "16x32") == 0) return 1;
+    if (e && strcmp(e, "16x16") == 0) return 2;
+    return 0;
   }();
-  return rg;
+  return v;
 }
+static int rec_rows() { return rec_layout() == 0 ? 32 : 16; }
+static int rec_units() { return rec_layout() == 1 ? 32 : 16; }
 
 size_t rec_layer_granule_bytes(int B) {
   const int Bp = (B + 31) / 32 * 32;
   return (size_t)3 * 2 * Bp * H * sizeof(uint32_t);
 }
 
-int rec_layer_waves() { return rec_rg() / 4; }
+int rec_layer_waves() { return rec_rows() * rec_units() / 64; }
 
-int rec_layer_grid_blocks(int B) { return (H / 16) * ((B + rec_rg() - 1) / rec_rg()) * 2; }
+int rec_layer_producers() { return H / rec_units(); }
 
-hipError_t rec_layer_occupancy(int* blocks_per_cu) {
+int rec_layer_grid_blocks(int B) { return (H / rec_units()) * ((B + rec_rows() - 1) / rec_rows()) * 2; }
+
+template <int RG, int UW>
+static hipError_t occ(int* n) {
   // both arithmetic variants must fit: the capacity is the smaller of the two
   int a = 0, b = 0;
-  hipError_t e = rec_rg() == 16
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rec_layer_kernel<16, false>, 256, 0)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rec_layer_kernel<32, false>, 512, 0);
-  if (e == hipSuccess)
-    e = rec_rg() == 16 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rec_layer_kernel<16, true>, 256, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rec_layer_kernel<32, true>, 512, 0);
-  *blocks_per_cu = a < b ? a : b;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rec_layer_kernel<RG, UW, false>, RG * UW, 0);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rec_layer_kernel<RG, UW, true>, RG * UW, 0);
+  *n = a < b ? a : b;
   return e;
+}
+
+hipError_t rec_layer_occupancy(int* blocks_per_cu) {
+  switch (rec_layout()) {
+    case 1: return occ<16, 32>(blocks_per_cu);
+    case 2: return occ<16, 16>(blocks_per_cu);
+    default: return occ<32, 16>(blocks_per_cu);
+  }
 }
 
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
@@ -293,21 +324,23 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s) {
-  const int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for either RG
-  const int RG = rec_rg();
-  dim3 grid(H / 16, (B + RG - 1) / RG, 2);
-  auto go = [&](auto kern, int threads) {
-    static const int fastcell = [] {
-      const char* e = std::getenv("CASR_REC_FASTCELL");
-      return e && std::atoi(e) == 1 ? 1 : 0;
-    }();
-    hipLaunchKernelGGL(kern, grid, dim3(threads), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens, B, Bp, Tp,
-                       residual, err, trace, fastcell);
+  const int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for every layout
+  const int RG = rec_rows(), UW = rec_units();
+  const int nrg = (B + RG - 1) / RG;
+  dim3 grid((H / UW) * nrg * 2);
+  static const int fastcell = [] {  // CASR_REC_FASTCELL=1: hardware-exp cell (tuning knob)
+    const char* e = std::getenv("CASR_REC_FASTCELL");
+    return e && std::atoi(e) == 1 ? 1 : 0;
+  }();
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(RG * UW), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens, B, Bp, Tp,
+                       residual, err, trace, fastcell, nrg);
   };
-  if (RG == 16)
-    s16 ? go(rec_layer_kernel<16, true>, 256) : go(rec_layer_kernel<16, false>, 256);
-  else
-    s16 ? go(rec_layer_kernel<32, true>, 512) : go(rec_layer_kernel<32, false>, 512);
+  switch (rec_layout()) {
+    case 1: s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>); break;
+    case 2: s16 ? go(rec_layer_kernel<16, 16, true>) : go(rec_layer_kernel<16, 16, false>); break;
+    default: s16 ? go(rec_layer_kernel<32, 16, true>) : go(rec_layer_kernel<32, 16, false>); break;
+  }
   return hipGetLastError();
 }
 

@@ -29,8 +29,8 @@ def main(B=256, T=800, path="/tmp/rec_trace.bin"):
     torch.cuda.synchronize()
     del os.environ["CASR_REC_TRACE"]
     raw = np.fromfile(path, dtype=np.uint32)
-    nwg, nw, Tp, ne = (int(x) for x in raw[:4].view(np.int32))
-    tr = raw[4:].reshape(nwg, nw, Tp, ne).astype(np.int64)
+    nwg, nw, Tp, ne, npg = (int(x) for x in raw[:5].view(np.int32))
+    tr = raw[5:].reshape(nwg, nw, Tp, ne).astype(np.int64)
     t = tr[..., :4] * 10.0 / 1000.0  # us
     t = t - t[..., 0:1, 0:1].min()
     ns = Tp - 1
@@ -39,10 +39,10 @@ def main(B=256, T=800, path="/tmp/rec_trace.bin"):
     cell = t[:, :, 1:, 3] - t[:, :, 1:, 2]
     period = t[:, :, 2:, 0] - t[:, :, 1:-1, 0]
     passes = tr[:, :, 1:, 4]
-    # grid order: blockIdx.x = 16 unit blocks, then row groups, then directions
-    ngrp = nwg // 16  # (row group, direction) groups of 16 producer workgroups
-    st = t[:, :, :, 3].max(axis=1).reshape(ngrp, 16, Tp)          # WG's last store per step
-    done = t[:, :, :, 1].reshape(ngrp, 16, nw, Tp)
+    # grid order: blockIdx.x = npg unit blocks, then row groups, then directions
+    ngrp = nwg // npg  # (row group, direction) groups of npg producer workgroups
+    st = t[:, :, :, 3].max(axis=1).reshape(ngrp, npg, Tp)          # WG's last store per step
+    done = t[:, :, :, 1].reshape(ngrp, npg, nw, Tp)
     lat = done[:, :, :, 1:] - st.max(axis=1)[:, None, None, :-1]
     total = t[:, :, -1, 3].max() - t[:, :, 0, 0].min()
     print(f"grid {nwg} WGs x {nw} waves, Tp={Tp}; layer wall {total:.1f} us = {total / Tp:.2f} us/step")
