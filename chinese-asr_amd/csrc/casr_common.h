@@ -100,8 +100,10 @@ CASR_DEV float wave_sum(float v) {
   return v;
 }
 
-// Hardware-exp forms (v_exp_f32 / v_rcp_f32): relative error ~|x| 1e-7 for the sigmoid, absolute
-// error ~1e-7 for tanh (diagnostic variant of the cell, CASR_REC_FASTCELL)
+// Hardware-exp forms (v_exp_f32 / v_rcp_f32): the exp2 argument rounding gives exp a relative
+// error ~|x| 6e-8, which the sigmoid's slope damps (absolute error <~1e-8); tanh = (1-e)/(1+e),
+// e = exp(-2|x|), has absolute error ~1e-7.  Used by the encoder cell in s16x3 arithmetic (the
+// f32 arithmetic keeps the libm cell below).
 CASR_DEV float sigmoid_hw(float x) { return __frcp_rn(1.0f + __expf(-x)); }
 CASR_DEV float tanh_hw(float x) {
   const float e = __expf(-2.f * fabsf(x));

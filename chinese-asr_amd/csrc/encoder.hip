@@ -444,7 +444,10 @@ __global__ __launch_bounds__(256) void rec_step_kernel(
     gate[tn] = sum + gin_v[tn];
   }
   float h2, c2;
-  lstm_cell(gate[0], gate[1], gate[2], gate[3], c_old, h2, c2);
+  if constexpr (S16)  // the persistent kernel's cell, bit for bit
+    lstm_cell_hw(gate[0], gate[1], gate[2], gate[3], c_old, h2, c2);
+  else
+    lstm_cell(gate[0], gate[1], gate[2], gate[3], c_old, h2, c2);
   cst[si] = c2;
   hnext[si] = h2;
   if (step == len - 1) hfin[si] = h2;

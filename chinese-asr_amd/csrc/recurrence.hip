@@ -82,7 +82,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
-    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int fastcell, int nrg) {
+    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg) {
   constexpr int NW = RG * UW / 64;      // waves: 4 k-chunks x RG/16 row halves x UW/16 unit halves
   __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
@@ -247,9 +247,9 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
         gate[tn] = sum + gin_v[tn];
       }
       float c2;
-      if (fastcell)
+      if constexpr (S16)  // performance arithmetic: hardware-exp cell (casr_common.h, ~1e-7)
         lstm_cell_hw(gate[0], gate[1], gate[2], gate[3], c, h2, c2);
-      else
+      else  // f32 arithmetic: libm cell, torch's CPU formulas
         lstm_cell(gate[0], gate[1], gate[2], gate[3], c, h2, c2);
       c = c2;
       const int t = (d == 0) ? s : (len - 1 - s);
@@ -328,13 +328,9 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
   const int RG = rec_rows(), UW = rec_units();
   const int nrg = (B + RG - 1) / RG;
   dim3 grid((H / UW) * nrg * 2);
-  static const int fastcell = [] {  // CASR_REC_FASTCELL=1: hardware-exp cell (tuning knob)
-    const char* e = std::getenv("CASR_REC_FASTCELL");
-    return e && std::atoi(e) == 1 ? 1 : 0;
-  }();
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(RG * UW), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens, B, Bp, Tp,
-                       residual, err, trace, fastcell, nrg);
+                       residual, err, trace, nrg);
   };
   switch (rec_layout()) {
     case 1: s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>); break;
