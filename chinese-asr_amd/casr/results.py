@@ -31,9 +31,46 @@ def edit_distance(a, b):
     return prev[n]
 
 
-def get_wer(pred, ref):
-    """util.py:237-249 with normalize=True: distance / len(ref)."""
-    return edit_distance(pred, ref) / (1.0 * len(ref))
+def edit_ops(pred, ref):
+    """(insert, delete, replace) counts of one minimal edit script turning ``pred`` into ``ref``
+    (python-Levenshtein ``editops(pred, ref)`` semantics, util.py:250-256).  The total always equals
+    the distance; how it splits into the three kinds depends on the backtrace's tie order, which
+    here prefers replace, then delete, then insert.  python-Levenshtein is absent (no fixture):
+    the split is parity-unpinned, the total is exact."""
+    m, n = len(pred), len(ref)
+    d = np.zeros((m + 1, n + 1), np.int64)
+    d[:, 0] = np.arange(m + 1)
+    d[0, :] = np.arange(n + 1)
+    for i in range(1, m + 1):
+        for j in range(1, n + 1):
+            d[i, j] = d[i - 1, j - 1] if pred[i - 1] == ref[j - 1] else \
+                1 + min(d[i - 1, j - 1], d[i - 1, j], d[i, j - 1])
+    i, j, ins, dele, rep = m, n, 0, 0, 0
+    while i > 0 or j > 0:
+        if i > 0 and j > 0 and pred[i - 1] == ref[j - 1] and d[i, j] == d[i - 1, j - 1]:
+            i, j = i - 1, j - 1
+        elif i > 0 and j > 0 and d[i, j] == d[i - 1, j - 1] + 1:
+            rep += 1
+            i, j = i - 1, j - 1
+        elif i > 0 and d[i, j] == d[i - 1, j] + 1:
+            dele += 1
+            i -= 1
+        else:
+            ins += 1
+            j -= 1
+    return ins, dele, rep
+
+
+def get_wer(pred, ref, normalize=True, return_tuple=False):
+    """util.py:237-262: distance(pred, ref) [/ len(ref)]; return_tuple: (all, insert, delete,
+    replace) [/ len(ref)] from the edit script (edit_ops)."""
+    n = len(ref) * 1.
+    if not return_tuple:
+        r = edit_distance(pred, ref)
+        return r / n if normalize else r
+    ins, dele, rep = edit_ops(pred, ref)
+    r = (ins + dele + rep, ins, dele, rep)
+    return tuple(e / n for e in r) if normalize else r
 
 
 def greedy_outputs(tokens, out_len, finished, accum):

@@ -132,3 +132,48 @@ def test_main_parse_and_asr_dropin(tmp_path):
     assert [asr(p) for p in paths] == want
     assert MN.parse_batch(paths, asr.model, asr.audio_base) == want
     assert isinstance(M.Model().load(ckpt), dict)
+
+
+def test_eval_loader_and_dataset_wer(tmp_path):
+    """Batch I/O for dataset-level WER: manifest -> AudioDst (eval) ->
+    AudioLoader batches through the HIP front-end with the loader's CMVN eps 1e-7
+    (data.py:515-518) -> evaluate (model.py:240-261).  Features match the oracle chain; the
+    dataset WER is the batch-size-weighted mean of the per-utterance WERs."""
+    import data as D
+    import model as M
+    from casr.results import get_wer
+    from casr.vocab import load_vocab
+    w2i, i2w = load_vocab()
+    ns = [24000, 40000, 12000, 30000, 20000]
+    refs = ["你好世界", "今天天气很好", "谢谢", "我们", "中国人民"]
+    lines, samples = [], []
+    for b, n in enumerate(ns):
+        p = tmp_path / f"u{b}.wav"
+        samples.append(_wav_file(p, synth_wav(n, 700 + b)))
+        lines.append(f"{p},{refs[b]}")
+    man = tmp_path / "dev.csv"
+    man.write_text("\n".join(lines))  # last line without newline: its text has no <unk>
+    ab = D.AudioBase(manifests={"dev": str(man)})
+    dst = D.AudioDst(ab, mode="eval", dev_or_test="dev")
+    loader = D.AudioLoader(dst, batch_size=2)
+    got, lens_all, texts = [], [], []
+    for t, lens, text in loader.loader:
+        assert isinstance(t, list) and lens.dtype == torch.int32
+        got += [x.cpu().numpy() for x in t]
+        lens_all += lens.tolist()
+        texts += text
+    assert len(got) == len(ns)
+    for b, s in enumerate(samples):
+        ref = O.cmvn(O.stack_frames(O.add_delta_deltas(O.log_mel(s))), 1e-7)
+        assert got[b].shape == ref.shape and lens_all[b] == ref.shape[0]
+        np.testing.assert_allclose(got[b], ref, atol=5e-3, rtol=0)
+    assert texts[-1] == [w2i.get(ch, w2i["<unk>"]) for ch in refs[-1]]
+    m = M.Model()
+    m.load_state_dicts(*synthetic_state_dicts(CFG, peaked=True))
+    wer, preds, rtexts = D.evaluate(m, loader, i2w)
+    assert len(preds) == len(ns)
+    per = [get_wer(p, r) for p, r in zip(preds, rtexts)]
+    np.testing.assert_allclose(wer, np.mean(per), rtol=1e-12)
+    # the same utterances one at a time give the same hypotheses (batch invariance)
+    one = D.AudioLoader(dst, batch_size=1)
+    assert D.evaluate(m, one, i2w)[1] == preds

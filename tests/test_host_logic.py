@@ -111,3 +111,67 @@ def test_checkpoint_roundtrip_with_reference_trainvar(tmp_path):
         for k in a:
             np.testing.assert_array_equal(a[k], b[k])
     assert args.step == 12000 and abs(args.best_wer - 0.06328) < 1e-12 and args.num_no_imprv == 2
+
+
+def _brute_distance(a, b):
+    """Levenshtein distance by plain recursion (tiny strings only): the definition."""
+    from functools import lru_cache
+
+    @lru_cache(maxsize=None)
+    def d(i, j):
+        if i == 0:
+            return j
+        if j == 0:
+            return i
+        return min(d(i - 1, j) + 1, d(i, j - 1) + 1, d(i - 1, j - 1) + (a[i - 1] != b[j - 1]))
+    return d(len(a), len(b))
+
+
+def test_wer_tuple_and_distance_definition():
+    """get_wer(pred, ref, normalize, return_tuple) of util.py:237-262: the total equals the
+    distance by definition; the (insert, delete, replace) split is one minimal edit script."""
+    from casr.results import edit_ops
+    rs = np.random.RandomState(3)
+    for _ in range(200):
+        a = "".join(rs.choice(list("abcd"), rs.randint(0, 7)))
+        b = "".join(rs.choice(list("abcd"), rs.randint(1, 7)))
+        dist = _brute_distance(a, b)
+        assert edit_distance(a, b) == dist
+        ins, dele, rep = edit_ops(a, b)
+        assert ins + dele + rep == dist
+        assert len(a) + ins - dele == len(b)  # the script turns pred into ref
+        tot = get_wer(a, b, normalize=False, return_tuple=True)
+        assert tot == (dist, ins, dele, rep)
+        np.testing.assert_allclose(get_wer(a, b, return_tuple=True), [x / len(b) for x in tot])
+        assert get_wer(a, b, normalize=False) == dist
+    assert edit_ops("abc", "abxc") == (1, 0, 0)
+    assert edit_ops("abxc", "abc") == (0, 1, 0)
+    assert edit_ops("abc", "abd") == (0, 0, 1)
+
+
+def test_manifest_and_eval_dataset_host(tmp_path):
+    """get_wav_path_text_list_from_manifest (data.py:402-405) keeps the reference's parsing (text
+    up to the next comma, trailing newline included, which maps to <unk>); AudioBase manifests feed
+    AudioDst's eval / infer modes (data.py:409-466); train mode is out of scope."""
+    import pytest
+    import data as D
+    man = tmp_path / "dev.csv"
+    man.write_text("/a/u0.wav,你好\n/a/u1.wav,世界,extra\n")
+    paths, texts = D.get_wav_path_text_list_from_manifest(str(man))
+    assert paths == ["/a/u0.wav", "/a/u1.wav"]
+    assert texts == ["你好\n", "世界"]
+    ab = D.AudioBase(manifests={"dev": str(man)}, infer_paths=["/x.wav"])
+    dst = D.AudioDst(ab, mode="eval", dev_or_test="dev")
+    assert len(dst) == 2 and dst.text_list == texts
+    unk = ab.word2int["<unk>"]
+    ids = dst.text_ids(0)
+    assert ids[-1] == unk and len(ids) == 3
+    assert ids[:2] == [ab.word2int.get(ch, unk) for ch in "你好"]
+    inf = D.AudioDst(ab, mode="infer", dev_or_test=None)
+    assert inf.path_list == ["/x.wav"] and inf.text_list is None
+    with pytest.raises(NotImplementedError):
+        D.AudioDst(ab, mode="train")
+    with pytest.raises(ValueError):
+        D.AudioDst(D.AudioBase(), mode="eval", dev_or_test="test")
+    loader = D.AudioLoader(dst, batch_size=1)
+    assert len(loader) == 2 and loader.loader is loader
