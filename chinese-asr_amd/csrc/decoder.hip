@@ -18,28 +18,41 @@
 // device-side per-step counter every kernel checks, so the host never synchronises.
 #include <float.h>
 
+#include <type_traits>
+
 #include "casr_common.h"
 #include "casr_internal.h"
 
 namespace casr {
 
-// ------------------------------------------------------------------ decode GEMM (LDS-DMA)
+// ------------------------------------------------------------------ decode GEMM (LDS-DMA ring)
 // C[R][N] = A[R][K] . W^T for the decoder LSTMCell (K = 1280, N = 2048 gate rows) and the
-// vocabulary projection (K = 1024, N = 5056).  Block = 64 (or 32) rows x 64 columns, 8 waves:
-// 4 (2) row slabs of 16 x 2 (4) slices of every 64-deep k tile; the slices are added once at the
-// end in a fixed order.  Operand tiles
-// are staged global -> LDS by LDS-DMA (global_load_lds_dwordx4), double-buffered, so the next
-// tile's loads run under the current tile's MFMAs:
-//   * W tile: 4 MFMA-fragment-major blocks (16 rows x 64 k, [q][lane][4]) copied verbatim; a
+// vocabulary projection (K = 1024, N = 5056).  Block = BM = 16 WR rows x 16 NT columns, 8 waves:
+// WR row slabs of 16 x KQ = 8 / WR slices of every 64-deep k tile; the slices are added once at
+// the end in a fixed order.  Operand tiles are staged global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4) through a ring of S stage buffers, so S - 1 k tiles are in flight
+// while one is multiplied:
+//   * W tile: NT MFMA-fragment-major blocks (16 rows x 64 k, [q][lane][4]) copied verbatim; a
 //     lane's fragment read is lane-linear, conflict-free;
-//   * A tile: 64 rows x 64 k, 256-B rows, 16-B chunk c of row r at c ^ (r & 15) (XOR on the
+//   * A tile: BM rows x 64 k, 256-B rows, 16-B chunk c of row r at c ^ (r & 15) (XOR on the
 //     per-lane DMA source address, same XOR on the read).  The per-lane source address also
 //     performs the decoder's row gather (embedding row of tok[r], state row of src[r]).
+// At M = R = 256 rows this GEMM is bound by the bytes each CU pulls from L2 / MALL per k tile and
+// by their latency (compute per tile is a few hundred cycles), so the ring depth, not the MFMA,
+// sets its speed (cdna_hip_programming.md "Pipelining across barriers"):
+//   * the S stage buffers are S distinct __shared__ arrays and the k loop is unrolled by S, so
+//     each ds_read names one of them and hipcc's own wait before it counts only the DMA into
+//     that array (one array with a runtime offset waits for every DMA in flight: the prefetch
+//     is serialised);
+//   * no __syncthreads() inside the loop (its fence drains every DMA in flight with vmcnt(0)):
+//     each wave retires its own DMA of tile kt with a counted s_waitcnt vmcnt, then a raw
+//     s_barrier makes everyone's part of tile kt visible and proves tile kt-1's buffer is no
+//     longer read, and only then is tile kt+S-1 issued into that buffer.
 // Grid: 1-D, XCD-aware.  Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md
 // "Workgroup dispatch": speed only, never correctness), so linear id L runs on XCD L % 8.  All
-// NR row blocks of one 64-column weight slice get ids with the same L % 8: the slice is
-// fetched into one XCD's L2 once and re-read from there by every row block.
-constexpr int DG_BK = 64, DG_TILE = 64 * DG_BK;  // W tile: 64 columns x 64 k
+// NR row blocks of one weight column slice get ids with the same L % 8: the slice is fetched into
+// one XCD's L2 once and re-read from there by every row block.
+constexpr int DG_BK = 64;
 
 __device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
   const int L = blockIdx.x, x = L & 7, j = L >> 3;
@@ -50,42 +63,97 @@ __device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
 
 inline unsigned xcd_grid(int NB, int NR) { return (unsigned)(8 * ((NB + 7) / 8) * NR); }
 
+// global_load_lds_dwordx4 in inline asm: hipcc does not see these DMAs, so it inserts no wait of
+// its own for them (seen, every ds_read of the ring waited vmcnt(0): the DMAs carry no alias
+// scope); the kernel orders them itself with counted vmcnt waits + s_barrier.  M0 = the wave's
+// LDS destination base (lane l writes base + 16 l), saved and restored around the load.
 __device__ __forceinline__ void lds_dma16(const float* src, float* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds_wave_base);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
 }
 
-// WR row slabs of 16 (block = 16 WR rows x 64 columns), KQ = 8 / WR waves split each 64-deep k
-// tile by MFMA step q (wave kq takes q in [kq * 4/KQ, (kq+1) * 4/KQ)); partials are added in kq order.
-// The two stage buffers are two distinct __shared__ arrays and the k loop is unrolled by 2 so every
-// ds_read names one of them: hipcc then proves the in-flight DMA (into the other array) does not
-// alias the read and does not drain it with vmcnt(0) (one array with a runtime index did: the
-// prefetch was serialised).  Each lane's A source rows are resolved once before the loop (an
-// ordinary load beside in-flight DMA also forces vmcnt(0)).
+// s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt[3:0], expcnt 7, lgkmcnt 15, vmcnt[5:4] << 14)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// wait until at most n (wave-uniform, 0 <= n) of this wave's vector-memory operations remain
+template <int MAXN>
+__device__ __forceinline__ void vm_wait_le(int n) {
+  if constexpr (MAXN == 0) {
+    vm_wait<0>();
+  } else {
+    if (n >= MAXN) vm_wait<MAXN>();
+    else vm_wait_le<MAXN - 1>(n);
+  }
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 // S16: A rows are split words (split16_word: [emb16 | ctx16 | h16]) and W is the s16 fragment
 // image (pack_frag16); a 64-deep tile is 2 k-steps of v_mfma_f32_16x16x32_f16 (s16x3), k-step
 // js = 2 kt + j going to wave kq = js % KQ.  Lane (r, g) of step j reads A words 16g + 8j .. +7
 // (two swizzled 16-B chunks) and W block [j][hi|lo][lane].
-template <int WR, class ASrc, class Epi, bool S16 = false>
-__global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, const float* __restrict__ Wf,
-                                                    ASrc asrc, Epi epi) {
-  constexpr int KQ = 8 / WR, QPW = 4 / KQ, BM = 16 * WR, ATILE = BM * DG_BK;
-  constexpr int NA = BM / 4, NDMA = NA + 16;  // DMA instructions per stage: A (4 rows each) + W
-  constexpr int NSLOT = (NDMA + 7) / 8;      // per wave
-  __shared__ __attribute__((aligned(16))) float buf0[ATILE + DG_TILE];  // [A tile | W tile]
-  __shared__ __attribute__((aligned(16))) float buf1[ATILE + DG_TILE];
+// ntiles: 16-row W fragment blocks that exist; a block's tiles past it re-read the last one (their
+// columns are discarded by the epilogue).
+template <int WR, int NT, int S, class ASrc, class Epi, bool S16 = false>
+__global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntiles, int nkt,
+                                                    const float* __restrict__ Wf, ASrc asrc, Epi epi) {
+  constexpr int KQ = 8 / WR, QPW = 4 / KQ, BM = 16 * WR, ATILE = BM * DG_BK, WTILE = NT * FRAG;
+  constexpr int STG = ATILE + WTILE;          // floats per stage: [A tile | W tile]
+  constexpr int NA = BM / 4, NDMA = NA + 4 * NT;  // DMA instructions per stage: A (4 rows each) + W
+  constexpr int NSLOT = (NDMA + 7) / 8;      // per wave (at most)
+  static_assert(S >= 2 && S <= 6, "ring of 2..6 stage buffers");
+  static_assert(S * STG * 4 <= 160 * 1024, "ring fits the LDS");
+  static_assert((S - 2) * NSLOT < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) float lb0[STG];
+  __shared__ __attribute__((aligned(16))) float lb1[STG];
+  __shared__ __attribute__((aligned(16))) float lb2[S > 2 ? STG : 4];
+  __shared__ __attribute__((aligned(16))) float lb3[S > 3 ? STG : 4];
+  __shared__ __attribute__((aligned(16))) float lb4[S > 4 ? STG : 4];
+  __shared__ __attribute__((aligned(16))) float lb5[S > 5 ? STG : 4];
+  auto buf = [&](auto I) -> float* {
+    if constexpr (I == 0) return lb0;
+    else if constexpr (I == 1) return lb1;
+    else if constexpr (I == 2) return lb2;
+    else if constexpr (I == 3) return lb3;
+    else if constexpr (I == 4) return lb4;
+    else return lb5;
+  };
   if (epi.skip()) return;
   int nb, rb;
   if (!xcd_tile(NB, NR, nb, rb)) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ws = w % WR, kq = w / WR;
   const int r = lane & 15, g = lane >> 4;
+  const int cnt_w = w < NDMA ? (NDMA - w + 7) / 8 : 0;  // DMA instructions this wave issues per stage
 
-  // per-lane DMA sources that do not depend on k: A row segment bases, W fragment offsets
+  // per-lane DMA sources that do not depend on k: A row segment bases, W fragment block bases
   const float* aseg[NSLOT][2];
+  const float* wsrc[NSLOT];
 #pragma unroll
   for (int j = 0; j < NSLOT; ++j) {
     const int i = w + 8 * j;
-    aseg[j][0] = aseg[j][1] = nullptr;
-    if (i < NA) asrc.bind(rb * BM + 4 * i + (lane >> 4), aseg[j][0], aseg[j][1]);
+    aseg[j][0] = aseg[j][1] = wsrc[j] = nullptr;
+    if (i < NA) {
+      asrc.bind(rb * BM + 4 * i + (lane >> 4), aseg[j][0], aseg[j][1]);
+    } else if (i < NDMA) {
+      const int tn = (i - NA) >> 2, qq = (i - NA) & 3;
+      int t = nb * NT + tn;
+      t = t < ntiles ? t : ntiles - 1;
+      wsrc[j] = Wf + (size_t)t * nkt * FRAG + qq * 256 + lane * 4;
+    }
   }
   auto stage = [&](float* dst, int kt) {
     float* la = dst;
@@ -100,14 +168,14 @@ __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, 
         lds_dma16(src + c * 4, la + i * 256);
       } else if (i < NDMA) {
         const int tn = (i - NA) >> 2, qq = (i - NA) & 3;
-        lds_dma16(Wf + ((size_t)(nb * 4 + tn) * nkt + kt) * FRAG + qq * 256 + lane * 4, lw + tn * FRAG + qq * 256);
+        lds_dma16(wsrc[j] + (size_t)kt * FRAG, lw + tn * FRAG + qq * 256);
       }
     }
   };
 
-  f32x4 acc[4], accx[4];
+  f32x4 acc[NT], accx[NT];
 #pragma unroll
-  for (int tn = 0; tn < 4; ++tn) acc[tn] = accx[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int tn = 0; tn < NT; ++tn) acc[tn] = accx[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int arow = ws * 16 + r;
   auto compute = [&](const float* src, int kt) {
     const float* la = src;
@@ -122,7 +190,7 @@ __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, 
         f16x8 ah, al;
         unpack16(w0, w1, ah, al);
 #pragma unroll
-        for (int tn = 0; tn < 4; ++tn) {
+        for (int tn = 0; tn < NT; ++tn) {
           const f16x8 bh = *reinterpret_cast<const f16x8*>(lw + tn * FRAG + (2 * j) * 256 + lane * 4);
           const f16x8 bl = *reinterpret_cast<const f16x8*>(lw + tn * FRAG + (2 * j + 1) * 256 + lane * 4);
           mfma_s16(ah, al, bh, bl, acc[tn], accx[tn]);
@@ -134,11 +202,11 @@ __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, 
     for (int qh = 0; qh < QPW; ++qh) {
       const int q = kq * QPW + qh;
       const float4 a = *reinterpret_cast<const float4*>(la + arow * DG_BK + (((4 * g + q) ^ (arow & 15)) << 2));
-      float4 b[4];
+      float4 b[NT];
 #pragma unroll
-      for (int tn = 0; tn < 4; ++tn) b[tn] = *reinterpret_cast<const float4*>(lw + tn * FRAG + q * 256 + lane * 4);
+      for (int tn = 0; tn < NT; ++tn) b[tn] = *reinterpret_cast<const float4*>(lw + tn * FRAG + q * 256 + lane * 4);
 #pragma unroll
-      for (int tn = 0; tn < 4; ++tn) {
+      for (int tn = 0; tn < NT; ++tn) {
         acc[tn] = mfma16x16x4(a.x, b[tn].x, acc[tn]);
         acc[tn] = mfma16x16x4(a.y, b[tn].y, acc[tn]);
         acc[tn] = mfma16x16x4(a.z, b[tn].z, acc[tn]);
@@ -146,61 +214,60 @@ __global__ __launch_bounds__(512, 4) void dgemm_kernel(int NB, int NR, int nkt, 
       }
     }
   };
-  stage(buf0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; kt += 2) {
-    if (kt + 1 < nkt) stage(buf1, kt + 1);
-    compute(buf0, kt);
-    __syncthreads();  // retires this wave's DMA into buf1 and everyone's reads of buf0
-    if (kt + 1 >= nkt) break;
-    if (kt + 2 < nkt) stage(buf0, kt + 2);
-    compute(buf1, kt + 1);
-    __syncthreads();
+
+  static_for<0, S - 1>([&](auto I) {
+    if (I < nkt) stage(buf(I), I);
+  });
+  for (int kt0 = 0; kt0 < nkt; kt0 += S) {
+    static_for<0, S>([&](auto I) {
+      const int kt = kt0 + I;
+      if (kt >= nkt) return;
+      // this wave's DMA of tile kt is done once at most (tiles issued after it) x cnt_w remain
+      const int ahead = min(S - 2, nkt - 1 - kt);
+      vm_wait_le<(S - 2) * NSLOT>(ahead * cnt_w);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of tile kt-1 are done
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");  // no LDS read of tile kt moves above the barrier
+      if (kt + S - 1 < nkt) stage(buf(std::integral_constant<int, (I + S - 1) % S>{}), kt + S - 1);
+      compute(buf(I), kt);
+    });
   }
+  __syncthreads();  // nothing in flight any more: every wave is done reading the ring
   if constexpr (S16) {
 #pragma unroll
-    for (int tn = 0; tn < 4; ++tn)
+    for (int tn = 0; tn < NT; ++tn)
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[tn][e] = s16_combine(acc[tn][e], accx[tn][e]);
   }
-  // k slices 1..KQ-1 hand their partial sums to slice 0 through LDS (free after the last barrier)
-  f32x4* part = reinterpret_cast<f32x4*>(buf0);
-  static_assert((KQ - 1) * WR * 4 * 64 * 16 <= (ATILE + DG_TILE) * 4, "partials fit one stage buffer");
-  if (kq > 0) {
+  // k slices 1..KQ-1 hand their partial sums to slice 0 through LDS (the ring is free now)
+  if constexpr (KQ > 1) {
+    f32x4* part = reinterpret_cast<f32x4*>(lb0);
+    static_assert((KQ - 1) * WR * NT * 64 * 16 <= STG * 4, "partials fit one stage buffer");
+    if (kq > 0) {
 #pragma unroll
-    for (int tn = 0; tn < 4; ++tn) part[(((kq - 1) * WR + ws) * 4 + tn) * 64 + lane] = acc[tn];
+      for (int tn = 0; tn < NT; ++tn) part[(((kq - 1) * WR + ws) * NT + tn) * 64 + lane] = acc[tn];
+    }
+    __syncthreads();
+    if (kq > 0) return;
+#pragma unroll
+    for (int j = 0; j < KQ - 1; ++j)
+#pragma unroll
+      for (int tn = 0; tn < NT; ++tn) acc[tn] += part[((j * WR + ws) * NT + tn) * 64 + lane];
   }
-  __syncthreads();
-  if (kq > 0) return;
-#pragma unroll
-  for (int j = 0; j < KQ - 1; ++j)
-#pragma unroll
-    for (int tn = 0; tn < 4; ++tn) acc[tn] += part[((j * WR + ws) * 4 + tn) * 64 + lane];
-  // lane holds rows rb*BM + ws*16 + 4g + e (e = 0..3), column nb*64 + tn*16 + r
-  epi.template run<4>(acc, rb * BM + ws * 16 + 4 * g, nb, r);
+  // lane holds rows rb*BM + ws*16 + 4g + e (e = 0..3), column (nb*NT + tn)*16 + r
+  epi.template run<NT>(acc, rb * BM + ws * 16 + 4 * g, nb, r);
 }
 
-// 64-row blocks where that still gives >= 2 blocks per CU, else 32-row blocks
-template <class ASrc, class Epi>
-static void launch_dgemm(int NB, int R, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi, int s16,
-                         hipStream_t s) {
-  const int NR64 = (R + 63) / 64;
-  if ((int)xcd_grid(NB, NR64) >= 512) {
-    if (s16)
-      hipLaunchKernelGGL((dgemm_kernel<4, ASrc, Epi, true>), dim3(xcd_grid(NB, NR64)), dim3(512), 0, s, NB, NR64,
-                         nkt, Wf, asrc, epi);
-    else
-      hipLaunchKernelGGL((dgemm_kernel<4, ASrc, Epi, false>), dim3(xcd_grid(NB, NR64)), dim3(512), 0, s, NB, NR64,
-                         nkt, Wf, asrc, epi);
-  } else {
-    const int NR32 = (R + 31) / 32;
-    if (s16)
-      hipLaunchKernelGGL((dgemm_kernel<2, ASrc, Epi, true>), dim3(xcd_grid(NB, NR32)), dim3(512), 0, s, NB, NR32,
-                         nkt, Wf, asrc, epi);
-    else
-      hipLaunchKernelGGL((dgemm_kernel<2, ASrc, Epi, false>), dim3(xcd_grid(NB, NR32)), dim3(512), 0, s, NB, NR32,
-                         nkt, Wf, asrc, epi);
-  }
+template <int WR, int NT, int S, class ASrc, class Epi>
+static void launch_dg(int NB, int R, int ntiles, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi,
+                      int s16, hipStream_t s) {
+  const int NR = (R + 16 * WR - 1) / (16 * WR);
+  if (s16)
+    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s, NB, NR,
+                       ntiles, nkt, Wf, asrc, epi);
+  else
+    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, false>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s, NB,
+                       NR, ntiles, nkt, Wf, asrc, epi);
 }
 
 // A rows of the decoder LSTM: [embed(tok[r]) | st_old[src[r]][0:1024] = ctx | h]; a 64-deep
@@ -253,8 +320,8 @@ struct DecLstmEpi {
   template <int NTN = 4>
   __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u) const {
     static_assert(NTN == 4, "the LSTM cell needs the 4 gate tiles of a 64-column block");
-    __shared__ float ht[4][16][17];  // per row-slab wave: h tile [row][unit]
-    const int lane = threadIdx.x & 63, ws = (row0 >> 4) & 3, g = lane >> 4;
+    __shared__ float ht[8][16][17];  // per row-slab wave (<= 8 per block): h tile [row][unit]
+    const int lane = threadIdx.x & 63, ws = (row0 >> 4) & 7, g = lane >> 4;
     const int U = nb * 16 + u;
     float bg[4];
 #pragma unroll
@@ -790,6 +857,33 @@ __global__ void beam_records_kernel(int B, int k, int L, const int32_t* __restri
   for (int s = l; s < L; ++s) o[s] = -1;
 }
 
+// ------------------------------------------------------------------ decode GEMM launch shapes
+// Tile choice per row count (one 512-thread block per CU, 256 blocks at R = 256):
+//   LSTMCell (N = 2048, 16 units x 4 gates per block): R <= 256: 32 rows, ring 4; R <= 512:
+//   64 rows, ring 4; else 128 rows, ring 3.
+//   projection (N = 5056 = 316 16-column tiles): R <= 256: 64 rows x 80 columns, ring 4;
+//   else 128 x 80, ring 3 (<= 156 KB of LDS each).
+// Measured at R = 256 (bench, ms per greedy batch of 40 steps): projection 64 x 80 ring 4 0.88
+// against 1.11 for the 32 x 64 two-buffer tile of 640 blocks, 1.19 for 64 x 64 ring 4 (316
+// blocks), 1.59 for 32 x 64 ring 6 (LDS then admits one of its 2.5 blocks per CU); the LSTMCell
+// is 0.92 at ring 2, 4 and 6 alike: past one tile in flight a CU's intake from MALL/HBM-latency
+// sources does not grow with depth (about 26-35 GB/s per CU in every variant).
+template <class ASrc, class Epi>
+static void launch_dec_lstm(int R, const float* Wf, const ASrc& asrc, const Epi& epi, int s16, hipStream_t s) {
+  const int NB = HD / 16, ntiles = 4 * NB, nkt = KDEC / DG_BK;
+  if (R <= 256) launch_dg<2, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else if (R <= 512) launch_dg<4, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else launch_dg<8, 4, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+}
+
+template <class ASrc, class Epi>
+static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi, int s16,
+                        hipStream_t s) {
+  const int nkt = KPROJ / DG_BK, NB = (ntiles + 4) / 5;
+  if (R <= 256) launch_dg<4, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else launch_dg<8, 5, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+}
+
 // ------------------------------------------------------------------ host drivers
 static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
                               hipStream_t s) {
@@ -800,7 +894,7 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
     ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
     DecLstmA asrc{a.W + (a.s16 ? a.L.emb16 : a.L.emb), st_old, d.tok[l & 1], d.src[l & 1], d.err, R, a.V, a.s16};
     DecLstmEpi epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, a.W + a.L.w_hidden, d.qpart, R, l, total};
-    launch_dgemm(HD / 16, R, KDEC / DG_BK, a.W + (a.s16 ? a.L.dec_w16 : a.L.dec_w), asrc, epi, a.s16, s);
+    launch_dec_lstm(R, a.W + (a.s16 ? a.L.dec_w16 : a.L.dec_w), asrc, epi, a.s16, s);
   }
   hipError_t e;
   {
@@ -812,7 +906,7 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
     ProfScope ps(a.prof, CASR_K_PROJ, s);
     ProjA asrc{st_new, R, a.s16};
     ProjEpi epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total};
-    launch_dgemm(a.L.VP / 64, R, KPROJ / DG_BK, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, s);
+    launch_proj(R, a.L.VP / 16, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, s);
   }
   return hipGetLastError();
 }

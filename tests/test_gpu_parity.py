@@ -278,7 +278,8 @@ def test_batch_invariance_and_determinism(eng):
     eng.encode(feat[100:116].contiguous(), flen[100:116].contiguous())
     c = eng.greedy()["tokens"].cpu()
     assert torch.equal(a[100:116], c)
-    eng.encode(feat[:64].contiguous(), flen[:64].contiguous())
+    # 128 x 8 = 1024 beam rows (the 128-row decode GEMM tiles) against 16 x 8 = 128 (32 / 64 rows)
+    eng.encode(feat[:128].contiguous(), flen[:128].contiguous())
     r1 = eng.beam(8)
     t1 = r1["tokens"].cpu()
     eng.encode(feat[:16].contiguous(), flen[:16].contiguous())
