@@ -119,13 +119,109 @@ __global__ __launch_bounds__(256) void cmvn_kernel(float* __restrict__ feat,
     }
 }
 
+// One pass for the whole chain (stack + deltas + CMVN): grid (F / FM mel slabs, B), block
+// 4 x 144 threads = 144 output dimensions (3 channels x 3 stacked frames x FM = 16 mels) x 4
+// time phases.  The block's fbank columns (nf x 16 floats) are staged in LDS once; each thread
+// computes its dimension's delta features for its time phase once, into registers (NJ per
+// thread), and the three sweeps (mean, centred second moment, normalise + store) run from
+// there, instead of round-tripping the un-normalised rows through HBM (the two kernels above:
+// 654 MB of traffic at B = 256, T = 800; here 65 MB read + 196 MB written).  Every feature value
+// is computed with stack_kernel's arithmetic (same taps and tap order); the statistics use
+// cmvn_kernel's 4-phase fixed-order reduction.
+constexpr int FM = 16, FQ = 9 * FM, FPH = 4, FNJ = 68;  // FNJ x FPH >= Tp (T <= 816 frames)
+static_assert(F % FM == 0, "mel slabs tile the 80 mels");
+
+__global__ __launch_bounds__(FQ * FPH) void features_fused_kernel(const float* __restrict__ fbank,
+                                                                  const int32_t* __restrict__ frames, int T,
+                                                                  int Tp, float eps, float* __restrict__ feat,
+                                                                  int32_t* __restrict__ feat_len) {
+  extern __shared__ float xs[];  // [nf][FM]
+  __shared__ float part[FPH][FQ];
+  __shared__ float stat[2][FQ];
+  const int m0 = blockIdx.x * FM, b = blockIdx.y;
+  const int tid = threadIdx.x, q = tid % FQ, ph = tid / FQ;
+  const int nf = min(frames[b], T);
+  const int lp = nf / 3;
+  if (blockIdx.x == 0 && tid == 0) feat_len[b] = lp;
+  const float* x = fbank + (size_t)b * T * F + m0;
+  for (int i = tid; i < nf * (FM / 4); i += FQ * FPH) {
+    const int t = i / (FM / 4), c4 = i % (FM / 4);
+    *reinterpret_cast<float4*>(xs + t * FM + 4 * c4) = *reinterpret_cast<const float4*>(x + (size_t)t * F + 4 * c4);
+  }
+  __syncthreads();
+  // dimension q = (c * 3 + r) * FM + mm  ->  output column c*240 + r*80 + m0 + mm
+  const int cr = q / FM, mm = q % FM, c = cr / 3, r = cr % 3;
+  const int o = c * 3 * F + r * F + m0 + mm;
+  const DeltaTaps taps = make_taps();
+  const float* w = (c == 1) ? taps.d1 : taps.d2;
+  float vals[FNJ];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < FNJ; ++i) {
+    const int j = ph + FPH * i;
+    float v = 0.f;
+    if (j < lp) {
+      const int t = 3 * j + r;
+      if (c == 0) {
+        v = xs[t * FM + mm];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+          const int tt = t + k - 4;
+          const float xv = (tt >= 0 && tt < nf) ? xs[tt * FM + mm] : 0.f;
+          v = __fadd_rn(v, __fmul_rn(w[k], xv));
+        }
+      }
+      s += v;
+    }
+    vals[i] = v;
+  }
+  float mean = 0.f, den = 1.f;
+  if (eps >= 0.f) {
+    part[ph][q] = s;
+    __syncthreads();
+    if (ph == 0) stat[0][q] = ((part[0][q] + part[1][q]) + (part[2][q] + part[3][q])) / (float)lp;
+    __syncthreads();
+    mean = stat[0][q];
+    float s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < FNJ; ++i)
+      if (ph + FPH * i < lp) {
+        const float dv = vals[i] - mean;
+        s2 += dv * dv;
+      }
+    __syncthreads();  // everyone has read part before it is reused
+    part[ph][q] = s2;
+    __syncthreads();
+    if (ph == 0) {
+      const float var = ((part[0][q] + part[1][q]) + (part[2][q] + part[3][q])) / (float)(lp - 1);
+      stat[1][q] = sqrtf(var) + eps;
+    }
+    __syncthreads();
+    den = stat[1][q];
+  }
+  float* out = feat + (size_t)b * Tp * D + o;
+#pragma unroll
+  for (int i = 0; i < FNJ; ++i) {
+    const int j = ph + FPH * i;
+    if (j < Tp) out[(size_t)j * D] = (j < lp && eps >= 0.f) ? (vals[i] - mean) / den : vals[i];
+  }
+}
+
 hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int T, float eps,
                            float* feat, int32_t* feat_len, hipStream_t s) {
   const int Tp = T / 3;
   if (Tp <= 0 || B <= 0) return hipErrorInvalidValue;
+  // eps < 0: no CMVN (the stacked features get_log_mel returns, data.py:226-249)
+  if (Tp <= FNJ * FPH) {
+    const size_t shm = (size_t)T * FM * sizeof(float);
+    hipLaunchKernelGGL(features_fused_kernel, dim3(F / FM, B), dim3(FQ * FPH), shm, s, fbank, frames, T, Tp, eps,
+                       feat, feat_len);
+    return hipGetLastError();
+  }
+  // longer utterances: the two-pass kernels
   hipLaunchKernelGGL(stack_kernel, dim3(Tp, B), dim3(256), 0, s, fbank, frames, T, Tp, feat,
                      feat_len);
-  // eps < 0: no CMVN (the stacked features get_log_mel returns, data.py:226-249)
   if (eps >= 0.f)
     hipLaunchKernelGGL(cmvn_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, feat, feat_len, Tp, eps);
   return hipGetLastError();

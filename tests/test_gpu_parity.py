@@ -68,6 +68,18 @@ def test_features_match_oracle(eng):
     fb = torch.from_numpy(fbank_for(0, 101))[None].to(eng.device)
     f1, _ = eng.features(fb, torch.tensor([101], dtype=torch.int32, device=eng.device))
     np.testing.assert_allclose(f1[0].cpu().numpy(), G["feat_cmvn_T101"], atol=2e-5, rtol=0)
+    # T > 1024 frames (the block's fbank columns no longer fit 64 KB of LDS): two-pass kernels;
+    # eps < 0: stacked features without CMVN, both paths
+    for T in (1100, 640):
+        fr = [T, T - 7]
+        fb, frt = batch_fbank(fr, eng.device)
+        f2, _ = eng.features(fb, frt)
+        f3, _ = eng.features(fb, frt, eps=-1.0)
+        for b, t in enumerate(fr):
+            np.testing.assert_allclose(f2[b, :t // 3].cpu().numpy(), O.features_from_fbank(fbank_for(b, t)),
+                                       atol=2e-5, rtol=0)
+            np.testing.assert_allclose(f3[b, :t // 3].cpu().numpy(), O.stack_frames(O.add_delta_deltas(fbank_for(b, t))),
+                                       atol=1e-5, rtol=0)
 
 
 @pytest.mark.parametrize("name", ["plain", "peaked"])
