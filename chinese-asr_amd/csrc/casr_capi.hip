@@ -761,7 +761,9 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
                                      (uint64_t)(align != nullptr), (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->enc_out, (uint64_t)h->keysT.p,
                                      (uint64_t)h->hfin.p, (uint64_t)h->cst.p, (uint64_t)h->lens.p};
+  dg_trace_init();  // CASR_DG_TRACE diagnostics only (outside any capture)
   HIP_OK(h, run_graph(h, key, s, [&](hipStream_t cs) { return run_greedy(a, h->d, itok, ilen, ifin, iacc, ial, cs); }));
+  dg_trace_dump();  // CASR_DG_TRACE diagnostics only (no-op otherwise)
   HIP_OK(h, hipMemcpyAsync(tokens, itok, sizeof(int32_t) * B * L, hipMemcpyDeviceToDevice, s));
   HIP_OK(h, hipMemcpyAsync(out_len, ilen, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
   HIP_OK(h, hipMemcpyAsync(finished, ifin, B, hipMemcpyDeviceToDevice, s));

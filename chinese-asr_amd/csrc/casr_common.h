@@ -82,9 +82,14 @@ CASR_DEV float sigmoid_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // Decode early exit (model.py:578, :897-901): newdone[s] counts rows / utterances that
 // finished at step s; step l runs only while fewer than `total` finished before it.
+// rows finished before decode step l (the per-step counters of steps 0..l-1): one wave-wide
+// load per 64 steps and a shuffle reduction, not l dependent loads
 CASR_DEV int done_before(const int32_t* __restrict__ newdone, int l) {
+  const int lane = threadIdx.x & 63;
   int s = 0;
-  for (int i = 0; i < l; ++i) s += newdone[i];
+  for (int i0 = 0; i0 < l; i0 += 64) s += (i0 + lane < l) ? newdone[i0 + lane] : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   return s;
 }
 

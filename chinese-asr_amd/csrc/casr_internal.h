@@ -242,6 +242,8 @@ hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qp
                                  int32_t* newdone, int l, int total, hipStream_t s);
 size_t attention_smem_bytes(int k, int Tp);
 
+void dg_trace_init();  // decoder.hip, CASR_DG_TRACE diagnostics
+void dg_trace_dump();
 hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
                       uint8_t* finished, float* accum, float* align, hipStream_t s);
 hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float length_weight,

@@ -18,7 +18,10 @@
 // device-side per-step counter every kernel checks, so the host never synchronises.
 #include <float.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 #include "casr_common.h"
 #include "casr_internal.h"
@@ -94,6 +97,10 @@ __device__ __forceinline__ void vm_wait_le(int n) {
   }
 }
 
+// diagnostics (CASR_DG_TRACE=<file>, tools/probes/dg_trace.py): per-block s_memrealtime stamps of
+// the last decode GEMM launch of each class; null otherwise (one scalar load per block)
+__device__ uint32_t* g_dg_trace = nullptr;
+
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
@@ -132,14 +139,19 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
     else if constexpr (I == 4) return lb4;
     else return lb5;
   };
-  if (epi.skip()) return;
   int nb, rb;
   if (!xcd_tile(NB, NR, nb, rb)) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ws = w % WR, kq = w / WR;
+  uint32_t* dtr = g_dg_trace ? g_dg_trace + ((size_t)Epi::kTraceClass * 4096 + blockIdx.x) * 8 : nullptr;
+  auto stamp = [&](int i) {
+    if (dtr && tid == 0) dtr[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   const int r = lane & 15, g = lane >> 4;
   const int cnt_w = w < NDMA ? (NDMA - w + 7) / 8 : 0;  // DMA instructions this wave issues per stage
 
   // per-lane DMA sources that do not depend on k: A row segment bases, W fragment block bases
+  int bad = 0;
   const float* aseg[NSLOT][2];
   const float* wsrc[NSLOT];
 #pragma unroll
@@ -147,7 +159,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
     const int i = w + 8 * j;
     aseg[j][0] = aseg[j][1] = wsrc[j] = nullptr;
     if (i < NA) {
-      asrc.bind(rb * BM + 4 * i + (lane >> 4), aseg[j][0], aseg[j][1]);
+      asrc.bind(rb * BM + 4 * i + (lane >> 4), aseg[j][0], aseg[j][1], bad);
     } else if (i < NDMA) {
       const int tn = (i - NA) >> 2, qq = (i - NA) & 3;
       int t = nb * NT + tn;
@@ -218,6 +230,15 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   static_for<0, S - 1>([&](auto I) {
     if (I < nkt) stage(buf(I), I);
   });
+  // after the first ring stages are in flight: the epilogue's operands (bias, predecessor rows,
+  // W_hidden), loaded under the k loop, and the early-exit check (its wait also retires those
+  // stages: a skipped block leaves no DMA behind)
+  const int erow0 = rb * BM + ws * 16 + 4 * (lane >> 4);
+  typename Epi::Pre pre;
+  if (kq == 0) epi.prefetch(pre, erow0, nb, lane & 15, bad);
+  if (epi.skip()) return;
+  if (bad) atomicOr(epi.err_flags(), bad);
+  stamp(1);
   for (int kt0 = 0; kt0 < nkt; kt0 += S) {
     static_for<0, S>([&](auto I) {
       const int kt = kt0 + I;
@@ -229,10 +250,13 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");  // no LDS read of tile kt moves above the barrier
       if (kt + S - 1 < nkt) stage(buf(std::integral_constant<int, (I + S - 1) % S>{}), kt + S - 1);
+      if (kt == 0) stamp(2);
       compute(buf(I), kt);
     });
   }
   __syncthreads();  // nothing in flight any more: every wave is done reading the ring
+  stamp(3);
+  if (kq == 0) epi.late(pre, erow0, nb, lane & 15);  // dependent loads, under the k-slice exchange
   if constexpr (S16) {
 #pragma unroll
     for (int tn = 0; tn < NT; ++tn)
@@ -255,7 +279,8 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       for (int tn = 0; tn < NT; ++tn) acc[tn] += part[((j * WR + ws) * NT + tn) * 64 + lane];
   }
   // lane holds rows rb*BM + ws*16 + 4g + e (e = 0..3), column (nb*NT + tn)*16 + r
-  epi.template run<NT>(acc, rb * BM + ws * 16 + 4 * g, nb, r);
+  epi.template run<NT>(acc, erow0, nb, r, pre);
+  stamp(4);
 }
 
 template <int WR, int NT, int S, class ASrc, class Epi>
@@ -281,33 +306,26 @@ struct DecLstmA {
   const int32_t* src;
   int32_t* err;
   int R, V, s16;
-  __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1) const {
+  // branch-free (a branch on a loaded index would serialise the prologue's loads: one round
+  // trip each); bad indices are clamped and reported through `bad` (CASR_DEV_* bits)
+  __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1, int& bad) const {
     row = row < R ? row : R - 1;
-    int t = tok[row];
-    if ((unsigned)t >= (unsigned)V) {
-      atomicOr(err, CASR_DEV_BAD_TOKEN);
-      t = 0;
-    }
-    seg0 = emb + (size_t)t * E;
-    seg1 = st_old + (size_t)safe_src(row) * ST + (s16 ? ST16 : 0);
+    const int t = tok[row];
+    const bool bt = (unsigned)t >= (unsigned)V;
+    bad |= bt ? CASR_DEV_BAD_TOKEN : 0;
+    seg0 = emb + (size_t)(bt ? 0 : t) * E;
+    seg1 = st_old + (size_t)safe_src(row, bad) * ST + (s16 ? ST16 : 0);
   }
-  __device__ __forceinline__ int safe_src(int row) const {
+  __device__ __forceinline__ int safe_src(int row, int& bad) const {
     const int s = src[row];
-    if ((unsigned)s >= (unsigned)R) {
-      atomicOr(err, CASR_DEV_BAD_SRC);
-      return row;
-    }
-    return s;
+    const bool bs = (unsigned)s >= (unsigned)R;
+    bad |= bs ? CASR_DEV_BAD_SRC : 0;
+    return bs ? row : s;
   }
 };
 
-// LSTMCell epilogue: the 4 n-tiles of a 64-column block are the 4 gates of 16 hidden units
-// (gate-interleaved packing), so each lane holds all four gates of its (row, unit) cells.
-// It also starts the attention query (attention.py:92, q = h . W_hidden): the wave's 16 x 16
-// tile of h (16 rows x this block's 16 units) times W_hidden[16 units][A] is one partial of q,
-// written to qpart[nb][row] (the attention kernel adds the HD/16 partials in a fixed order).
-// The tile is transposed through LDS into the A operand of 32 exact-f32 MFMAs (16x16x4).
 struct DecLstmEpi {
+  static constexpr int kTraceClass = 0;
   const float* bias;  // packed [4HD]
   const float* st_old;
   float* st_new;
@@ -316,23 +334,46 @@ struct DecLstmEpi {
   const float* w_hidden;  // [HD][A]
   float* qpart;           // [HD/16][R][A]
   int R, l, total;
+  // operands loaded before the k loop: gate biases, predecessor rows, this lane's W_hidden
+  // fragments of the query partial (A/16 x 4 MFMA steps); c of the predecessor after it
+  struct Pre {
+    float bg[4];
+    int srow[4];
+    float wh[A / 16][4];
+    float cold[4];
+  };
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
+  __device__ __forceinline__ int32_t* err_flags() const { return rows.err; }
+  __device__ __forceinline__ void prefetch(Pre& p, int row0, int nb, int u, int& bad) const {
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+#pragma unroll
+    for (int gt = 0; gt < 4; ++gt) p.bg[gt] = bias[nb * 64 + gt * 16 + u];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p.srow[e] = rows.safe_src(min(row0 + e, R - 1), bad);
+    const float* wp = w_hidden + (size_t)(nb * 16 + g) * A + (lane & 15);
+#pragma unroll
+    for (int at = 0; at < A / 16; ++at)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) p.wh[at][kk] = wp[(size_t)(4 * kk) * A + at * 16];
+  }
+  __device__ __forceinline__ void late(Pre& p, int row0, int nb, int u) const {
+    const int U = nb * 16 + u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) p.cold[e] = st_old[(size_t)p.srow[e] * ST + C + HD + U];
+  }
   template <int NTN = 4>
-  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u) const {
+  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p) const {
     static_assert(NTN == 4, "the LSTM cell needs the 4 gate tiles of a 64-column block");
     __shared__ float ht[8][16][17];  // per row-slab wave (<= 8 per block): h tile [row][unit]
     const int lane = threadIdx.x & 63, ws = (row0 >> 4) & 7, g = lane >> 4;
     const int U = nb * 16 + u;
-    float bg[4];
-#pragma unroll
-    for (int gt = 0; gt < 4; ++gt) bg[gt] = bias[nb * 64 + gt * 16 + u];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int row = row0 + e;
       float h2 = 0.f, c2;
       if (row < R) {
-        lstm_cell(acc[0][e] + bg[0], acc[1][e] + bg[1], acc[2][e] + bg[2], acc[3][e] + bg[3],
-                  st_old[(size_t)rows.safe_src(row) * ST + C + HD + U], h2, c2);
+        lstm_cell(acc[0][e] + p.bg[0], acc[1][e] + p.bg[1], acc[2][e] + p.bg[2], acc[3][e] + p.bg[3], p.cold[e], h2,
+                  c2);
         st_new[(size_t)row * ST + C + U] = h2;
         st_new[(size_t)row * ST + C + HD + U] = c2;
         reinterpret_cast<uint32_t*>(st_new)[(size_t)row * ST + ST16 + C + U] = split16_word(h2);
@@ -342,13 +383,11 @@ struct DecLstmEpi {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read back by other lanes of this wave
     __builtin_amdgcn_wave_barrier();
     const int rbase = row0 - 4 * g;  // first row of this wave's slab
-    const float* wp = w_hidden + (size_t)(nb * 16 + g) * A + (lane & 15);
 #pragma unroll
     for (int at = 0; at < A / 16; ++at) {
       f32x4 q = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-        q = mfma16x16x4(ht[ws][lane & 15][4 * kk + g], wp[(size_t)(4 * kk) * A + at * 16], q);
+      for (int kk = 0; kk < 4; ++kk) q = mfma16x16x4(ht[ws][lane & 15][4 * kk + g], p.wh[at][kk], q);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = rbase + 4 * g + e;
@@ -362,27 +401,42 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
   static constexpr int kSeg = 0;
   const float* st;
   int R, s16;
-  __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1) const {
+  __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1, int&) const {
     seg0 = seg1 = st + (size_t)(row < R ? row : R - 1) * ST + (s16 ? ST16 : 0);
   }
 };
 
 struct ProjEpi {
+  static constexpr int kTraceClass = 1;
   const float* bias;
   float* logits;
   const int32_t* newdone;
   int R, V, l, total;
+  struct Pre {
+    float bn[8];
+  };
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
+  int32_t* err;
+  __device__ __forceinline__ int32_t* err_flags() const { return err; }
+  __device__ __forceinline__ void prefetch(Pre& p, int, int nb, int u, int&) const {
+    // NTN = 5 columns tiles per block in every launch shape (launch_proj)
+#pragma unroll
+    for (int tn = 0; tn < 5; ++tn) {
+      const int n = (nb * 5 + tn) * 16 + u;
+      p.bn[tn] = n < V ? bias[n] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void late(Pre&, int, int, int) const {}
   template <int NTN = 4>
-  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u) const {
+  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p) const {
+    static_assert(NTN == 5, "prefetch assumes 5 column tiles per block");
 #pragma unroll
     for (int tn = 0; tn < NTN; ++tn) {
       const int n = (nb * NTN + tn) * 16 + u;
       if (n >= V) continue;
-      const float bn = bias[n];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        if (row0 + e < R) logits[(size_t)(row0 + e) * V + n] = acc[tn][e] + bn;
+        if (row0 + e < R) logits[(size_t)(row0 + e) * V + n] = acc[tn][e] + p.bn[tn];
     }
   }
 };
@@ -905,10 +959,39 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   {
     ProfScope ps(a.prof, CASR_K_PROJ, s);
     ProjA asrc{st_new, R, a.s16};
-    ProjEpi epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total};
+    ProjEpi epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total, d.err};
     launch_proj(R, a.L.VP / 16, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, s);
   }
   return hipGetLastError();
+}
+
+// CASR_DG_TRACE=<file>: allocate the stamp buffer once and point g_dg_trace at it (diagnostics)
+static uint32_t* dg_trace_buffer() {
+  static uint32_t* buf = nullptr;
+  static bool init = false;
+  if (!init) {
+    init = true;
+    if (std::getenv("CASR_DG_TRACE") && hipMalloc(&buf, 2 * 4096 * 8 * sizeof(uint32_t)) == hipSuccess) {
+      (void)hipMemset(buf, 0, 2 * 4096 * 8 * sizeof(uint32_t));
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dg_trace), &buf, sizeof(buf));
+    }
+  }
+  return buf;
+}
+
+void dg_trace_init() { dg_trace_buffer(); }
+
+void dg_trace_dump() {
+  uint32_t* buf = dg_trace_buffer();
+  const char* path = std::getenv("CASR_DG_TRACE");
+  if (!buf || !path) return;
+  std::vector<uint32_t> h(2 * 4096 * 8);
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpy(h.data(), buf, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  if (FILE* f = std::fopen(path, "wb")) {
+    std::fwrite(h.data(), 4, h.size(), f);
+    std::fclose(f);
+  }
 }
 
 hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,

@@ -1,0 +1,39 @@
+"""Per-block phase stamps of the decode GEMMs (CASR_DG_TRACE diagnostics; GPU box).
+
+One greedy decode at B x T; the stamps of the last launch of each GEMM class (s_memrealtime,
+100 MHz) are split into prologue (row binding + first ring stages issued), first tile landed,
+k loop, epilogue."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "chinese-asr_amd"))
+PATH = "/tmp/dg_trace.bin"
+os.environ["CASR_DG_TRACE"] = PATH
+from casr.config import CasrConfig  # noqa: E402
+from casr.engine import Engine  # noqa: E402
+from casr.weights import synthetic_state_dicts  # noqa: E402
+
+B, T = int(os.environ.get("B", 256)), 800
+cfg = CasrConfig()
+eng = Engine(cfg, *synthetic_state_dicts(cfg, peaked=True, eos_bias=0.0))
+fb = torch.from_numpy(np.stack([np.random.RandomState(1234 + b).standard_normal((T, 80)).astype(np.float32)
+                                for b in range(B)])).cuda()
+feat, flen = eng.features(fb, torch.full((B,), T, dtype=torch.int32, device="cuda"))
+eng.encode(feat, flen)
+eng.greedy()["tokens"].cpu()
+eng.greedy()["tokens"].cpu()
+raw = np.fromfile(PATH, dtype=np.uint32).reshape(2, 4096, 8).astype(np.int64)
+for cls, name in ((0, "dec_lstm"), (1, "proj")):
+    r = raw[cls]
+    r = r[r[:, 0] > 0]
+    t = (r[:, :5] - r[:, 0].min()) * 10 / 1000.0  # us
+    span = t[:, 4].max()
+    ph = {"start": t[:, 0], "prologue": t[:, 1] - t[:, 0], "first tile": t[:, 2] - t[:, 1],
+          "k loop": t[:, 3] - t[:, 2], "epilogue": t[:, 4] - t[:, 3], "block": t[:, 4] - t[:, 0]}
+    print(f"{name}: {len(r)} blocks, span {span:.2f} us")
+    for k, v in ph.items():
+        print(f"  {k:12s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f}")
