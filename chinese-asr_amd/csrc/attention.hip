@@ -52,7 +52,7 @@ template <int KPB>
 __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float* __restrict__ st, const float* __restrict__ qpart, const float* __restrict__ keysT,
     const float* __restrict__ enc, const int32_t* __restrict__ lens, const float* __restrict__ vv, int R, int k,
-    int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l, int total) {
+    int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l, int total, int npf) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ float wred[2][AT_WAVES][KPB];
   if (done_before(newdone, l) >= total) return;
@@ -61,6 +61,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   float* vs = qs + KPB * A;        // [A]
   float* xs = vs + A;              // scratch
   float* es = xs + attn_scratch_floats<KPB>(Tq);  // [KPB][Tq]
+  float* vl = es + KPB * Tq;                       // [npf][C]: value rows 0..npf-1 (LDS-DMA)
   const int b = blockIdx.x, j0 = blockIdx.y * KPB;
   const int nk = min(KPB, k - j0);
   const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
@@ -88,41 +89,76 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
   const int apg = (A + G - 1) / G;
   const float* kb = keysT + (size_t)b * A * Tq;
-  for (int it = tid; it < G * nch; it += AT_THREADS) {
+  constexpr int CH = 20;  // keys rows in flight per batch (apg = 19 at Tp = 266)
+  // this thread's score work: (a-group, 4-step chunk) items it = tid, tid + 512, ...; each in
+  // batches of CH keys rows
+  auto score_item = [&](int it, bool first, auto&& after_loads) {
     const int ag = it / nch, c = it - ag * nch, t0 = 4 * c;
     const int a0 = ag * apg, a1 = min(A, a0 + apg);
+    const bool live = it < G * nch && t0 < len;
     float e4[KPB][4];
 #pragma unroll
     for (int j = 0; j < KPB; ++j) e4[j][0] = e4[j][1] = e4[j][2] = e4[j][3] = 0.f;
-    if (t0 < len) {
-      constexpr int CH = 20;  // keys rows in flight per batch (apg = 19 at Tp = 266)
-      for (int ab = a0; ab < a1; ab += CH) {
-        float4 kv[CH];
+    auto batch = [&](const float4 (&kv)[CH], int ab) {
 #pragma unroll
-        for (int i = 0; i < CH; ++i)
-          kv[i] = ab + i < a1 ? *reinterpret_cast<const float4*>(kb + (size_t)(ab + i) * Tq + t0)
-                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int i = 0; i < CH; ++i) {
+        if (ab + i >= a1) break;
+        const float va = vs[ab + i];
 #pragma unroll
-        for (int i = 0; i < CH; ++i) {
-          if (ab + i >= a1) break;
-          const float va = vs[ab + i];
-#pragma unroll
-          for (int j = 0; j < KPB; ++j)
-            if (j < nk) {
-              const float qa = qs[j * A + ab + i];
-              e4[j][0] = __fadd_rn(e4[j][0], __fmul_rn(tanh_fast(kv[i].x + qa), va));
-              e4[j][1] = __fadd_rn(e4[j][1], __fmul_rn(tanh_fast(kv[i].y + qa), va));
-              e4[j][2] = __fadd_rn(e4[j][2], __fmul_rn(tanh_fast(kv[i].z + qa), va));
-              e4[j][3] = __fadd_rn(e4[j][3], __fmul_rn(tanh_fast(kv[i].w + qa), va));
-            }
-        }
+        for (int j = 0; j < KPB; ++j)
+          if (j < nk) {
+            const float qa = qs[j * A + ab + i];
+            e4[j][0] = __fadd_rn(e4[j][0], __fmul_rn(tanh_fast(kv[i].x + qa), va));
+            e4[j][1] = __fadd_rn(e4[j][1], __fmul_rn(tanh_fast(kv[i].y + qa), va));
+            e4[j][2] = __fadd_rn(e4[j][2], __fmul_rn(tanh_fast(kv[i].z + qa), va));
+            e4[j][3] = __fadd_rn(e4[j][3], __fmul_rn(tanh_fast(kv[i].w + qa), va));
+          }
       }
-    }
+    };
+    auto load = [&](float4 (&kv)[CH], int ab) {
 #pragma unroll
-    for (int j = 0; j < KPB; ++j)
-      if (j < nk)
-        *reinterpret_cast<float4*>(xs + (ag * KPB + j) * Tq + t0) = make_float4(e4[j][0], e4[j][1], e4[j][2], e4[j][3]);
-  }
+      for (int i = 0; i < CH; ++i)
+        kv[i] = live && ab + i < a1 ? *reinterpret_cast<const float4*>(kb + (size_t)(ab + i) * Tq + t0)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    int ab = a0;
+    if (first) {  // straight-line first batch: no loop join between its wait and its use
+      float4 kv[CH];
+      load(kv, ab);
+      after_loads();
+      if (live) batch(kv, ab);
+      ab += CH;
+    }
+    for (; live && ab < a1; ab += CH) {
+      float4 kv[CH];
+      load(kv, ab);
+      batch(kv, ab);
+    }
+    if (live)
+#pragma unroll
+      for (int j = 0; j < KPB; ++j)
+        if (j < nk)
+          *reinterpret_cast<float4*>(xs + (ag * KPB + j) * Tq + t0) = make_float4(e4[j][0], e4[j][1], e4[j][2], e4[j][3]);
+  };
+  // The first batch of keys is loaded and waited for by every wave (a wait hipcc sees), then the
+  // value rows 0..npf-1 go to LDS by LDS-DMA (inline asm, hipcc does not see it) and stream in
+  // while the block computes tanh scores and the softmax: the chip's HBM is otherwise idle in
+  // those phases, since every block runs them at the same time.
+  const int nv = min(npf, len);
+  score_item(tid, true, [&]() {
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): the keys batch has landed
+    const uint32_t vbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)vl;
+    for (int i = wv; i < 2 * nv; i += AT_WAVES) {  // 1 KB (half a row) per wave instruction
+      const float* src = enc + ((size_t)b * Tp + (i >> 1)) * C + (i & 1) * (C / 2) + 4 * ln;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(vbase + (uint32_t)i * (C / 2) * 4);
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(src), "s"(dst)
+                   : "memory");
+    }
+  });
+  for (int it = tid + AT_THREADS; it < G * nch; it += AT_THREADS) score_item(it, false, [] {});
   __syncthreads();
 
   // combine the G group partials (fixed order), mask past len, row maxima
@@ -204,8 +240,25 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 #pragma unroll
     for (int j = 0; j < KPB; ++j) acc[j][0] = acc[j][1] = acc[j][2] = acc[j][3] = 0.f;
     const float* eb = enc + (size_t)b * Tp * C + 4 * c4;
+    // rows 0..nv-1 from LDS (the DMA issued in the score phase; nv is a multiple of 4 or len, so
+    // each thread's t sequence continues unchanged into the global rows: same summation order)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int t = tp;
+    for (; t < nv; t += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(vl + (size_t)t * C + 4 * c4);
+#pragma unroll
+      for (int j = 0; j < KPB; ++j)
+        if (j < nk) {
+          const float al = es[j * Tq + t];
+          acc[j][0] = __fadd_rn(acc[j][0], __fmul_rn(al, v.x));
+          acc[j][1] = __fadd_rn(acc[j][1], __fmul_rn(al, v.y));
+          acc[j][2] = __fadd_rn(acc[j][2], __fmul_rn(al, v.z));
+          acc[j][3] = __fadd_rn(acc[j][3], __fmul_rn(al, v.w));
+        }
+    }
     constexpr int CT = 32;
-    for (int tb = tp; tb < len; tb += 4 * CT) {
+    for (int tb = t; tb < len; tb += 4 * CT) {
       float4 v4[CT];
 #pragma unroll
       for (int i = 0; i < CT; ++i) {
@@ -249,10 +302,21 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   }
 }
 
+// value rows prefetched into LDS by each block: what fits beside the block's other LDS (160 KiB
+// per CU, one block per CU), a multiple of 4 rows
+template <int KPB>
+static int attn_npf(int Tp) {
+  const size_t fixed = attn_smem_floats<KPB>(Tp) * sizeof(float) + 2 * AT_WAVES * KPB * sizeof(float);
+  const size_t room = fixed < 156 * 1024 ? 156 * 1024 - fixed : 0;
+  const int rows = (int)(room / (C * sizeof(float))) & ~3;
+  return rows < Tp ? rows : (Tp + 3) & ~3;
+}
+
 template <int KPB>
 static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart, float* align, int32_t* newdone,
                              int l, int total, hipStream_t s) {
-  const size_t shm = attn_smem_floats<KPB>(a.Tp) * sizeof(float);
+  const int npf = attn_npf<KPB>(a.Tp);
+  const size_t shm = (attn_smem_floats<KPB>(a.Tp) + (size_t)npf * C) * sizeof(float);
   static size_t raised = 0;  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950)
   if (shm > raised) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(attention_kernel<KPB>),
@@ -262,7 +326,7 @@ static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart,
   }
   dim3 grid(a.B, (a.k + KPB - 1) / KPB);
   hipLaunchKernelGGL(attention_kernel<KPB>, grid, dim3(AT_THREADS), shm, s, st, qpart, a.keysT, a.enc, a.lens,
-                     a.W + a.L.v, a.B * a.k, a.k, a.Tp, align, newdone, l, total);
+                     a.W + a.L.v, a.B * a.k, a.k, a.Tp, align, newdone, l, total, npf);
   return hipGetLastError();
 }
 

@@ -235,6 +235,7 @@ struct DecodeArgs {
   float temperature;
   int s16;               // decoder GEMMs on the s16x3 images (casr_set_precision)
   Profiler* prof;        // may be null
+  int greedy_run;        // set by run_greedy: the projection writes per-block argmax partials
 };
 
 // attention.hip: one decode step's additive attention for all R rows (writes ctx into st)

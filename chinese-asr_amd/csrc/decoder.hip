@@ -406,18 +406,31 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
   }
 };
 
+// Greedy decoding needs, per row, only the first-index argmax of the logits and their
+// logsumexp (model.py:554-560), so in greedy mode the projection epilogue does not store the
+// R x V logits: each block reduces its 80 columns of each row to (max, first argmax, sum of
+// exp(x - max)) and writes that partial (GreedyPart); greedy_select_part_kernel combines the
+// 64 partials of a row.  Beam search keeps the full logits (logits != nullptr).
+constexpr int GP_NB = 64;  // column blocks of the projection (5 x 16 columns each): V <= 5120
+struct GreedyPart {
+  float* mx;    // [R][GP_NB]
+  float* se;    // [R][GP_NB]
+  int32_t* ix;  // [R][GP_NB]
+};
+
 struct ProjEpi {
   static constexpr int kTraceClass = 1;
   const float* bias;
-  float* logits;
+  float* logits;  // beam: [R][V]; nullptr in greedy mode (gp)
   const int32_t* newdone;
   int R, V, l, total;
+  int32_t* err;
+  GreedyPart gp;
   struct Pre {
     float bn[8];
   };
-  __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
-  int32_t* err;
   __device__ __forceinline__ int32_t* err_flags() const { return err; }
+  __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
   __device__ __forceinline__ void prefetch(Pre& p, int, int nb, int u, int&) const {
     // NTN = 5 columns tiles per block in every launch shape (launch_proj)
 #pragma unroll
@@ -430,13 +443,56 @@ struct ProjEpi {
   template <int NTN = 4>
   __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p) const {
     static_assert(NTN == 5, "prefetch assumes 5 column tiles per block");
+    if (logits) {
 #pragma unroll
-    for (int tn = 0; tn < NTN; ++tn) {
-      const int n = (nb * NTN + tn) * 16 + u;
-      if (n >= V) continue;
+      for (int tn = 0; tn < NTN; ++tn) {
+        const int n = (nb * NTN + tn) * 16 + u;
+        if (n >= V) continue;
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (row0 + e < R) logits[(size_t)(row0 + e) * V + n] = acc[tn][e] + p.bn[tn];
+        for (int e = 0; e < 4; ++e)
+          if (row0 + e < R) logits[(size_t)(row0 + e) * V + n] = acc[tn][e] + p.bn[tn];
+      }
+      return;
+    }
+    // greedy partials of rows row0 + e over this block's columns: lane (g, u) holds columns
+    // (nb*5 + tn)*16 + u; the 16 lanes of one g share the rows
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x[NTN];
+      float m = -INFINITY;
+      int mi = 0x7fffffff;
+#pragma unroll
+      for (int tn = 0; tn < NTN; ++tn) {
+        const int n = (nb * NTN + tn) * 16 + u;
+        x[tn] = acc[tn][e] + p.bn[tn];
+        if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
+          m = x[tn];
+          mi = n;
+        }
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const float om = __shfl_xor(m, o, 64);
+        const int oi = __shfl_xor(mi, o, 64);
+        if (om > m || (om == m && oi < mi)) {
+          m = om;
+          mi = oi;
+        }
+      }
+      float sx = 0.f;
+#pragma unroll
+      for (int tn = 0; tn < NTN; ++tn) {
+        const int n = (nb * NTN + tn) * 16 + u;
+        if (n < V) sx += expf(x[tn] - m);
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) sx += __shfl_xor(sx, o, 64);
+      const int row = row0 + e;
+      if (u == 0 && row < R) {
+        gp.mx[(size_t)row * GP_NB + nb] = m;
+        gp.se[(size_t)row * GP_NB + nb] = sx;
+        gp.ix[(size_t)row * GP_NB + nb] = mi;
+      }
     }
   }
 };
@@ -573,6 +629,66 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(
       fin[r] = 1;
       atomicAdd(&newdone[l], 1);
     }
+  }
+}
+
+// Greedy step from the projection's per-block partials (ProjEpi greedy mode): one wave per row,
+// lane b holds block b's (max, first argmax, sum exp(x - max)); the row's maximum takes the
+// lowest column among equal maxima (torch.argmax: first index), and the sum of exp(x - max) is
+// rebuilt as sum_b se_b exp(m_b - max) by a fixed shuffle tree.  Bookkeeping exactly as
+// greedy_select_kernel (model.py:540-590).
+__global__ __launch_bounds__(256) void greedy_select_part_kernel(
+    GreedyPart gp, int nbp, int V, int R, int l, int L, int eos, int32_t* __restrict__ tok_next,
+    int32_t* __restrict__ src_next, uint8_t* __restrict__ fin, int32_t* __restrict__ out_len, float* __restrict__ accum,
+    int32_t* __restrict__ tokens, int32_t* __restrict__ newdone, int32_t* __restrict__ err) {
+  if (done_before(newdone, l) >= R) return;
+  const int ln = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  float m = -INFINITY, se = 0.f;
+  int mi = 0x7fffffff;
+  if (ln < nbp) {
+    m = gp.mx[(size_t)r * GP_NB + ln];
+    se = gp.se[(size_t)r * GP_NB + ln];
+    mi = gp.ix[(size_t)r * GP_NB + ln];
+  }
+  float gm = m;
+  int gi = mi;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(gm, o, 64);
+    const int oi = __shfl_xor(gi, o, 64);
+    if (better(om, oi, gm, gi)) {
+      gm = om;
+      gi = oi;
+    }
+  }
+  float s = (se > 0.f) ? se * expf(m - gm) : 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (ln != 0) return;
+  const float lse = logf(s) + gm;
+  const float lp = gm - lse;
+  int tok = gi;
+  if ((unsigned)tok >= (unsigned)V) {  // no finite maximum (NaN row)
+    atomicOr(err, CASR_DEV_NAN_LOGITS);
+    tok = 0;
+  }
+  tokens[(size_t)r * L + l] = tok;
+  tok_next[r] = tok;
+  src_next[r] = r;
+  const bool was = fin[r] != 0;
+  const bool cur = tok == eos;
+  float acc = accum[r];
+  if (!was && cur) acc = acc + lp;  // model.py:567
+  const bool now = was || cur;
+  if (!now) {
+    out_len[r] += 1;  // model.py:573
+    acc = acc + lp;   // model.py:576
+  }
+  accum[r] = acc;
+  if (now && !was) {
+    fin[r] = 1;
+    atomicAdd(&newdone[l], 1);
   }
 }
 
@@ -939,6 +1055,12 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
 }
 
 // ------------------------------------------------------------------ host drivers
+// greedy mode of the projection epilogue: the vocabulary must fit the 64 partial blocks (and the
+// partials the logits buffer: 3 x 64 words per row <= V)
+static bool greedy_partials(const DecodeArgs& a) {
+  return (a.L.VP / 16 + 4) / 5 <= GP_NB && a.V >= 3 * GP_NB && a.greedy_run;
+}
+
 static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
                               hipStream_t s) {
   const int R = a.B * a.k;
@@ -959,7 +1081,10 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   {
     ProfScope ps(a.prof, CASR_K_PROJ, s);
     ProjA asrc{st_new, R, a.s16};
-    ProjEpi epi{a.W + a.L.proj_b, d.logits, d.newdone, R, a.V, l, total, d.err};
+    // greedy (k == 1 and not beam): per-block partials instead of logits
+    GreedyPart gp{d.logits, d.logits + (size_t)R * GP_NB, reinterpret_cast<int32_t*>(d.logits) + (size_t)2 * R * GP_NB};
+    const bool greedy = a.k == 1 && greedy_partials(a);
+    ProjEpi epi{a.W + a.L.proj_b, greedy ? nullptr : d.logits, d.newdone, R, a.V, l, total, d.err, gp};
     launch_proj(R, a.L.VP / 16, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, s);
   }
   return hipGetLastError();
@@ -994,8 +1119,10 @@ void dg_trace_dump() {
   }
 }
 
-hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
+hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
                       uint8_t* finished, float* accum, float* align, hipStream_t s) {
+  DecodeArgs a = a_in;
+  a.greedy_run = 1;
   const int R = a.B;
   // fill kernels, not hipMemsetAsync: this sequence is captured into a replayed graph
   hipError_t e0 = fill_u32(d.newdone, 0, a.max_len, s);
@@ -1011,9 +1138,16 @@ hipError_t run_greedy(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32
     hipError_t e = decode_step(a, d, l, R, align ? align + (size_t)l * a.Tp * R : nullptr, s);
     if (e != hipSuccess) return e;
     ProfScope ps(a.prof, CASR_K_SELECT, s);
-    hipLaunchKernelGGL(greedy_select_kernel, dim3(R), dim3(256), 0, s, d.logits, a.V, R, l,
-                       a.max_len, a.eos, d.tok[(l + 1) & 1], d.src[(l + 1) & 1], finished, out_len,
-                       accum, tokens, d.newdone, d.err);
+    if (greedy_partials(a)) {
+      GreedyPart gp{d.logits, d.logits + (size_t)R * GP_NB, reinterpret_cast<int32_t*>(d.logits) + (size_t)2 * R * GP_NB};
+      hipLaunchKernelGGL(greedy_select_part_kernel, dim3((R + 3) / 4), dim3(256), 0, s, gp, (a.L.VP / 16 + 4) / 5, a.V,
+                         R, l, a.max_len, a.eos, d.tok[(l + 1) & 1], d.src[(l + 1) & 1], finished, out_len, accum,
+                         tokens, d.newdone, d.err);
+    } else {
+      hipLaunchKernelGGL(greedy_select_kernel, dim3(R), dim3(256), 0, s, d.logits, a.V, R, l,
+                         a.max_len, a.eos, d.tok[(l + 1) & 1], d.src[(l + 1) & 1], finished, out_len,
+                         accum, tokens, d.newdone, d.err);
+    }
   }
   return hipGetLastError();
 }
