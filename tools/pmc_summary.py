@@ -20,11 +20,11 @@ CLASS_OF = {  # bench.py kernel classes -> kernel-name prefixes (after short())
     "input_proj": "gemm16_bias_kernel",
     "keys": "gemm_nt_kernel<KeysEpi>",
     "rec_step": "rec_layer_kernel",
-    "dec_lstm": "dgemm_kernel<2, DecLstmA",
-    "proj": "dgemm_kernel<2, ProjA",
+    "dec_lstm": "dgemm_kernel<2, 4, 4, DecLstmA",
+    "proj": "dgemm_kernel<4, 5, 4, ProjA",
     "attention": "attention_kernel<1>",
-    "select": "greedy_select_kernel",
-    "features": "cmvn_kernel",
+    "select": "greedy_select_part_kernel",
+    "features": "features_fused_kernel",
 }
 
 

@@ -16,15 +16,18 @@ def main(path, top=25):
     acc = defaultdict(list)
     with open(path) as f:
         for r in csv.DictReader(f):
-            name = r["Kernel_Name"]
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
             short = name[:name.index("(")] if "(" in name else name
             grid = tuple(int(r[f"Grid_Size_{a}"]) // max(1, int(r[f"Workgroup_Size_{a}"])) for a in "XYZ")
             wg = int(r["Workgroup_Size_X"]) * int(r["Workgroup_Size_Y"]) * int(r["Workgroup_Size_Z"])
             acc[(short, grid, wg)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     rows = sorted(acc.items(), key=lambda kv: -sum(kv[1]))
-    print(f"{'kernel':58s} {'workgroups (x,y,z) x threads':30s} {'calls':>6s} {'avg_us':>10s} {'total_ms':>9s}")
+    print(f"{'kernel':58s} {'workgroups (x,y,z) x threads':30s} {'calls':>6s} {'avg_us':>10s} {'median_us':>10s} "
+          f"{'total_ms':>9s}")
     for (name, grid, wg), d in rows[:top]:
-        print(f"{name[:58]:58s} {str(grid) + ' x ' + str(wg):30s} {len(d):6d} {sum(d) / len(d):10.2f} {sum(d) / 1e3:9.2f}")
+        med = sorted(d)[len(d) // 2]
+        print(f"{name[:58]:58s} {str(grid) + ' x ' + str(wg):30s} {len(d):6d} {sum(d) / len(d):10.2f} {med:10.2f} "
+              f"{sum(d) / 1e3:9.2f}")
 
 
 if __name__ == "__main__":
