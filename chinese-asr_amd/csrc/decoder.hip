@@ -761,7 +761,9 @@ __device__ __forceinline__ void wave_merge(TopList<K2>& L, int n, float* outv, i
 // the k*V flattened scores, model.py:860-865; ties -> lower flat index).
 constexpr int BS_CAP = 256;  // threshold candidates kept per row (beyond: full selection)
 
-template <int K2>
+// UNIT_T: temperature == 1 (the reference default, gpd['temperature']): x / T is x exactly, so the
+// three per-element divisions of each pass are skipped (bitwise the same values)
+template <int K2, bool UNIT_T>
 __global__ __launch_bounds__(512) void beam_select_kernel(
     const float* __restrict__ logits, int V, int B, int k, int l, int L, int eos, float temperature,
     const float* __restrict__ score_cur, float* __restrict__ score_next,
@@ -782,6 +784,7 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
   const int nrows = (l == 0) ? 1 : k;  // model.py:862-863: step 0 ranks beam 0 only
   const int n2k = 2 * k;
   const bool vec = (V & 3) == 0;
+  auto xt = [&](float x) { return UNIT_T ? x : x / temperature; };
 
   for (int j = wv; j < nrows; j += 8) {
     const float* x = logits + (size_t)(b * k + j) * V;
@@ -791,11 +794,11 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
 #pragma unroll 4
       for (int i = ln; i < V / 4; i += 64) {
         const float4 q = x4[i];
-        lm = fmaxf(lm, fmaxf(fmaxf(q.x / temperature, q.y / temperature),
-                             fmaxf(q.z / temperature, q.w / temperature)));
+        lm = fmaxf(lm, fmaxf(fmaxf(xt(q.x), xt(q.y)),
+                             fmaxf(xt(q.z), xt(q.w))));
       }
     } else {
-      for (int v = ln; v < V; v += 64) lm = fmaxf(lm, x[v] / temperature);
+      for (int v = ln; v < V; v += 64) lm = fmaxf(lm, xt(x[v]));
     }
     const float m = wave_max(lm);
     float s = 0.f;
@@ -803,11 +806,11 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
 #pragma unroll 4
       for (int i = ln; i < V / 4; i += 64) {
         const float4 q = x4[i];
-        s += expf(q.x / temperature - m) + expf(q.y / temperature - m) + expf(q.z / temperature - m) +
-             expf(q.w / temperature - m);
+        s += expf(xt(q.x) - m) + expf(xt(q.y) - m) + expf(xt(q.z) - m) +
+             expf(xt(q.w) - m);
       }
     } else {
-      for (int v = ln; v < V; v += 64) s += expf(x[v] / temperature - m);
+      for (int v = ln; v < V; v += 64) s += expf(xt(x[v]) - m);
     }
     s = wave_sum(s);
     const float lse = logf(s) + m;
@@ -839,13 +842,13 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
 #pragma unroll 2
       for (int i = ln; i < V / 4; i += 64) {
         const float4 q = x4[i];
-        offer((q.x / temperature - lse) + sc, j * V + 4 * i);
-        offer((q.y / temperature - lse) + sc, j * V + 4 * i + 1);
-        offer((q.z / temperature - lse) + sc, j * V + 4 * i + 2);
-        offer((q.w / temperature - lse) + sc, j * V + 4 * i + 3);
+        offer((xt(q.x) - lse) + sc, j * V + 4 * i);
+        offer((xt(q.y) - lse) + sc, j * V + 4 * i + 1);
+        offer((xt(q.z) - lse) + sc, j * V + 4 * i + 2);
+        offer((xt(q.w) - lse) + sc, j * V + 4 * i + 3);
       }
     } else {
-      for (int v = ln; v < V; v += 64) offer((x[v] / temperature - lse) + sc, j * V + v);
+      for (int v = ln; v < V; v += 64) offer((xt(x[v]) - lse) + sc, j * V + v);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -857,13 +860,13 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     } else if (vec) {  // more ties at tau than the buffer holds: every element
       for (int i = ln; i < V / 4; i += 64) {
         const float4 q = x4[i];
-        tl.insert((q.x / temperature - lse) + sc, j * V + 4 * i);  // model.py:834-836
-        tl.insert((q.y / temperature - lse) + sc, j * V + 4 * i + 1);
-        tl.insert((q.z / temperature - lse) + sc, j * V + 4 * i + 2);
-        tl.insert((q.w / temperature - lse) + sc, j * V + 4 * i + 3);
+        tl.insert((xt(q.x) - lse) + sc, j * V + 4 * i);  // model.py:834-836
+        tl.insert((xt(q.y) - lse) + sc, j * V + 4 * i + 1);
+        tl.insert((xt(q.z) - lse) + sc, j * V + 4 * i + 2);
+        tl.insert((xt(q.w) - lse) + sc, j * V + 4 * i + 3);
       }
     } else {
-      for (int v = ln; v < V; v += 64) tl.insert((x[v] / temperature - lse) + sc, j * V + v);
+      for (int v = ln; v < V; v += 64) tl.insert((xt(x[v]) - lse) + sc, j * V + v);
     }
     wave_merge<K2>(tl, n2k, rv_s[j], ri_s[j]);
   }
@@ -1154,7 +1157,8 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
 
 template <int K2>
 static void launch_beam_select(const DecodeArgs& a, DecodeBufs& d, int l, hipStream_t s) {
-  hipLaunchKernelGGL(beam_select_kernel<K2>, dim3(a.B), dim3(512), 0, s, d.logits, a.V, a.B, a.k, l,
+  auto kern = a.temperature == 1.0f ? beam_select_kernel<K2, true> : beam_select_kernel<K2, false>;
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(512), 0, s, d.logits, a.V, a.B, a.k, l,
                      a.max_len, a.eos, a.temperature, d.score[l & 1], d.score[(l + 1) & 1],
                      d.tok[(l + 1) & 1], d.src[(l + 1) & 1], d.topfin, d.bp, d.tk, d.rec_score,
                      d.rec_src, d.rec_valid, d.newdone, d.err);
