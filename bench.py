@@ -240,9 +240,15 @@ def main():
 
         step_beam()
         dtb = timed(step_beam, args.beam_steps)
+        # one instrumented beam step after the timed region: per-class milliseconds
+        eng.profile(["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"])
+        step_beam()
+        beam_breakdown = {c: round(v[1], 3) for c, v in eng.profile_read().items()}
+        eng.profile([])
         beam = {"k": args.beam, "batch_per_gpu": Bb, "value": Bb * world * args.beam_steps / dtb,
                 "unit": "utt/s", "ms_per_step": 1000.0 * dtb / args.beam_steps,
-                "rtf": dtb / args.beam_steps / (Bb * world * AUDIO_S_PER_UTT)}
+                "rtf": dtb / args.beam_steps / (Bb * world * AUDIO_S_PER_UTT),
+                "kernel_breakdown_ms": beam_breakdown}
 
     # side measurement: the same greedy step on the exact-f32 MFMA path (not the headline)
     f32_cmp = None

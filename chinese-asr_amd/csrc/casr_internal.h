@@ -203,9 +203,18 @@ hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, cons
                        float* keysT, hipStream_t s);
 
 // decoder.hip
+// projection column blocks (5 x 16 columns each) whose per-row partials the selects combine: V <= 5120
+constexpr int GP_NB = 64;
+struct GreedyPart {
+  float* mx;    // [R][GP_NB] block maximum of the row's logits
+  float* se;    // [R][GP_NB] sum exp(x - block maximum)
+  int32_t* ix;  // [R][GP_NB] first column of the block maximum
+};
+
 struct DecodeBufs {
   float* st[2];          // [R][ST]
   float* logits;         // [R][V]
+  GreedyPart part;       // per-block row partials of the projection (after the logits)
   float* qpart;          // [HD/16][R][A] attention query partials, one per 16-unit block of h
   int32_t* tok[2];       // [R]
   int32_t* src[2];       // [R]

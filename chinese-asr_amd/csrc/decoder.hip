@@ -411,17 +411,13 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
 // R x V logits: each block reduces its 80 columns of each row to (max, first argmax, sum of
 // exp(x - max)) and writes that partial (GreedyPart); greedy_select_part_kernel combines the
 // 64 partials of a row.  Beam search keeps the full logits (logits != nullptr).
-constexpr int GP_NB = 64;  // column blocks of the projection (5 x 16 columns each): V <= 5120
-struct GreedyPart {
-  float* mx;    // [R][GP_NB]
-  float* se;    // [R][GP_NB]
-  int32_t* ix;  // [R][GP_NB]
-};
 
 struct ProjEpi {
   static constexpr int kTraceClass = 1;
   const float* bias;
-  float* logits;  // beam: [R][V]; nullptr in greedy mode (gp)
+  float* logits;  // [R][V] (beam); nullptr in greedy mode
+  // per-block row partials (greedy; beam at temperature 1 for its logsumexp and threshold), or
+  // gp.mx == nullptr
   const int32_t* newdone;
   int R, V, l, total;
   int32_t* err;
@@ -452,8 +448,8 @@ struct ProjEpi {
         for (int e = 0; e < 4; ++e)
           if (row0 + e < R) logits[(size_t)(row0 + e) * V + n] = acc[tn][e] + p.bn[tn];
       }
-      return;
     }
+    if (!gp.mx) return;
     // greedy partials of rows row0 + e over this block's columns: lane (g, u) holds columns
     // (nb*5 + tn)*16 + u; the 16 lanes of one g share the rows
 #pragma unroll
@@ -770,7 +766,7 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     int32_t* __restrict__ tok_next, int32_t* __restrict__ src_next, uint8_t* __restrict__ topfin,
     int32_t* __restrict__ bp, int32_t* __restrict__ tk, float* __restrict__ rec_score,
     int32_t* __restrict__ rec_src, uint8_t* __restrict__ rec_valid, int32_t* __restrict__ newdone,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, GreedyPart gp, int nbp) {
   __shared__ float rv_s[KMAX_BEAM][K2];
   __shared__ int ri_s[KMAX_BEAM][K2];
   __shared__ float cv[K2];
@@ -789,38 +785,50 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
   for (int j = wv; j < nrows; j += 8) {
     const float* x = logits + (size_t)(b * k + j) * V;
     const float4* x4 = reinterpret_cast<const float4*>(x);
-    float lm = -INFINITY;  // this lane's largest x / T
-    if (vec) {
-#pragma unroll 4
-      for (int i = ln; i < V / 4; i += 64) {
-        const float4 q = x4[i];
-        lm = fmaxf(lm, fmaxf(fmaxf(xt(q.x), xt(q.y)),
-                             fmaxf(xt(q.z), xt(q.w))));
-      }
-    } else {
-      for (int v = ln; v < V; v += 64) lm = fmaxf(lm, xt(x[v]));
-    }
-    const float m = wave_max(lm);
-    float s = 0.f;
-    if (vec) {
-#pragma unroll 4
-      for (int i = ln; i < V / 4; i += 64) {
-        const float4 q = x4[i];
-        s += expf(xt(q.x) - m) + expf(xt(q.y) - m) + expf(xt(q.z) - m) +
-             expf(xt(q.w) - m);
-      }
-    } else {
-      for (int v = ln; v < V; v += 64) s += expf(xt(x[v]) - m);
-    }
-    s = wave_sum(s);
-    const float lse = logf(s) + m;
     const float sc = score_cur[b * k + j];
-    // Threshold filter for the row's top-2k (model.py:834-865 ranks val = (x/T - lse) + score):
-    // val is monotone in x, so a lane's largest val is (lm - lse) + sc, and the 2k-th largest of
-    // the 64 lane maxima, tau, bounds the row's 2k-th best val from below (those 2k maxima are
-    // distinct elements).  Only elements with val >= tau (typically a few dozen) enter the
-    // sorted-list selection, instead of every element in every lane (divergent insertions).
-    float lt = (lm - lse) + sc, tau = -INFINITY;
+    float lse, lt;  // the row's logsumexp; this lane's largest candidate value (for tau)
+    if (UNIT_T && nbp > 0) {
+      // from the projection's per-block partials (ProjEpi): lane c holds block c's max and
+      // sum exp(x - max); the 64 block maxima are distinct elements, so their 2k-th largest
+      // bounds the row's 2k-th best value from below just as the lane maxima do
+      float mb = -INFINITY, sb = 0.f;
+      if (ln < nbp) {
+        mb = gp.mx[(size_t)(b * k + j) * GP_NB + ln];
+        sb = gp.se[(size_t)(b * k + j) * GP_NB + ln];
+      }
+      const float M = wave_max(mb);
+      float s = (sb > 0.f) ? sb * expf(mb - M) : 0.f;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      lse = logf(s) + M;
+      lt = (mb - lse) + sc;
+    } else {
+      float lm = -INFINITY;  // this lane's largest x / T
+      if (vec) {
+#pragma unroll 4
+        for (int i = ln; i < V / 4; i += 64) {
+          const float4 q = x4[i];
+          lm = fmaxf(lm, fmaxf(fmaxf(xt(q.x), xt(q.y)), fmaxf(xt(q.z), xt(q.w))));
+        }
+      } else {
+        for (int v = ln; v < V; v += 64) lm = fmaxf(lm, xt(x[v]));
+      }
+      const float m = wave_max(lm);
+      float s = 0.f;
+      if (vec) {
+#pragma unroll 4
+        for (int i = ln; i < V / 4; i += 64) {
+          const float4 q = x4[i];
+          s += expf(xt(q.x) - m) + expf(xt(q.y) - m) + expf(xt(q.z) - m) + expf(xt(q.w) - m);
+        }
+      } else {
+        for (int v = ln; v < V; v += 64) s += expf(xt(x[v]) - m);
+      }
+      s = wave_sum(s);
+      lse = logf(s) + m;
+      lt = (lm - lse) + sc;
+    }
+    float tau = -INFINITY;
     for (int c = 0; c < n2k; ++c) {
       const float mx = wave_max(lt);
       tau = mx;
@@ -1058,10 +1066,10 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
 }
 
 // ------------------------------------------------------------------ host drivers
-// greedy mode of the projection epilogue: the vocabulary must fit the 64 partial blocks (and the
-// partials the logits buffer: 3 x 64 words per row <= V)
-static bool greedy_partials(const DecodeArgs& a) {
-  return (a.L.VP / 16 + 4) / 5 <= GP_NB && a.V >= 3 * GP_NB && a.greedy_run;
+// per-block row partials from the projection epilogue: the vocabulary must fit the 64 partial
+// blocks; beam search uses them at temperature 1 only (they are of x, not x / T)
+static bool row_partials(const DecodeArgs& a) {
+  return (a.L.VP / 16 + 4) / 5 <= GP_NB && (a.greedy_run || a.temperature == 1.0f);
 }
 
 static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
@@ -1084,10 +1092,10 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
   {
     ProfScope ps(a.prof, CASR_K_PROJ, s);
     ProjA asrc{st_new, R, a.s16};
-    // greedy (k == 1 and not beam): per-block partials instead of logits
-    GreedyPart gp{d.logits, d.logits + (size_t)R * GP_NB, reinterpret_cast<int32_t*>(d.logits) + (size_t)2 * R * GP_NB};
-    const bool greedy = a.k == 1 && greedy_partials(a);
-    ProjEpi epi{a.W + a.L.proj_b, greedy ? nullptr : d.logits, d.newdone, R, a.V, l, total, d.err, gp};
+    // greedy: per-block partials instead of logits; beam at temperature 1: logits and partials
+    const bool parts = row_partials(a);
+    const GreedyPart gp = parts ? d.part : GreedyPart{nullptr, nullptr, nullptr};
+    ProjEpi epi{a.W + a.L.proj_b, a.greedy_run && parts ? nullptr : d.logits, d.newdone, R, a.V, l, total, d.err, gp};
     launch_proj(R, a.L.VP / 16, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, s);
   }
   return hipGetLastError();
@@ -1141,9 +1149,8 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
     hipError_t e = decode_step(a, d, l, R, align ? align + (size_t)l * a.Tp * R : nullptr, s);
     if (e != hipSuccess) return e;
     ProfScope ps(a.prof, CASR_K_SELECT, s);
-    if (greedy_partials(a)) {
-      GreedyPart gp{d.logits, d.logits + (size_t)R * GP_NB, reinterpret_cast<int32_t*>(d.logits) + (size_t)2 * R * GP_NB};
-      hipLaunchKernelGGL(greedy_select_part_kernel, dim3((R + 3) / 4), dim3(256), 0, s, gp, (a.L.VP / 16 + 4) / 5, a.V,
+    if (row_partials(a)) {
+      hipLaunchKernelGGL(greedy_select_part_kernel, dim3((R + 3) / 4), dim3(256), 0, s, d.part, (a.L.VP / 16 + 4) / 5, a.V,
                          R, l, a.max_len, a.eos, d.tok[(l + 1) & 1], d.src[(l + 1) & 1], finished, out_len, accum,
                          tokens, d.newdone, d.err);
     } else {
@@ -1161,7 +1168,7 @@ static void launch_beam_select(const DecodeArgs& a, DecodeBufs& d, int l, hipStr
   hipLaunchKernelGGL(kern, dim3(a.B), dim3(512), 0, s, d.logits, a.V, a.B, a.k, l,
                      a.max_len, a.eos, a.temperature, d.score[l & 1], d.score[(l + 1) & 1],
                      d.tok[(l + 1) & 1], d.src[(l + 1) & 1], d.topfin, d.bp, d.tk, d.rec_score,
-                     d.rec_src, d.rec_valid, d.newdone, d.err);
+                     d.rec_src, d.rec_valid, d.newdone, d.err, d.part, row_partials(a) ? (a.L.VP / 16 + 4) / 5 : 0);
 }
 
 hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float length_weight,
