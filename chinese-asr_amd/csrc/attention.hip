@@ -334,6 +334,8 @@ hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qp
                                  int32_t* newdone, int l, int total, hipStream_t s) {
   if (a.k == 1) return launch_kpb<1>(a, st, qpart, align, newdone, l, total, s);
   if (a.k == 2) return launch_kpb<2>(a, st, qpart, align, newdone, l, total, s);
+  // k > 4 keeps 4 rows per block: 8 rows per block (one block per utterance, half the grid)
+  // measured 3.68 ms vs 2.87 ms per B = 128, k = 8 batch
   return launch_kpb<4>(a, st, qpart, align, newdone, l, total, s);
 }
 

@@ -235,7 +235,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   // stages: a skipped block leaves no DMA behind)
   const int erow0 = rb * BM + ws * 16 + 4 * (lane >> 4);
   typename Epi::Pre pre;
-  if (kq == 0) epi.prefetch(pre, erow0, nb, lane & 15, bad);
+  if (kq == 0) epi.template prefetch<NT>(pre, erow0, nb, lane & 15, bad);
   if (epi.skip()) return;
   if (bad) atomicOr(epi.err_flags(), bad);
   stamp(1);
@@ -344,6 +344,7 @@ struct DecLstmEpi {
   };
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
   __device__ __forceinline__ int32_t* err_flags() const { return rows.err; }
+  template <int NTN>
   __device__ __forceinline__ void prefetch(Pre& p, int row0, int nb, int u, int& bad) const {
     const int lane = threadIdx.x & 63, g = lane >> 4;
 #pragma unroll
@@ -423,22 +424,23 @@ struct ProjEpi {
   int32_t* err;
   GreedyPart gp;
   struct Pre {
-    float bn[8];
+    float bn[16];
   };
   __device__ __forceinline__ int32_t* err_flags() const { return err; }
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
+  template <int NTN>
   __device__ __forceinline__ void prefetch(Pre& p, int, int nb, int u, int&) const {
-    // NTN = 5 columns tiles per block in every launch shape (launch_proj)
+    static_assert(NTN <= 16, "bias prefetch slots");
 #pragma unroll
-    for (int tn = 0; tn < 5; ++tn) {
-      const int n = (nb * 5 + tn) * 16 + u;
+    for (int tn = 0; tn < NTN; ++tn) {
+      const int n = (nb * NTN + tn) * 16 + u;
       p.bn[tn] = n < V ? bias[n] : 0.f;
     }
   }
   __device__ __forceinline__ void late(Pre&, int, int, int) const {}
   template <int NTN = 4>
   __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p) const {
-    static_assert(NTN == 5, "prefetch assumes 5 column tiles per block");
+    static_assert(NTN <= 16, "bias prefetch slots");
     if (logits) {
 #pragma unroll
       for (int tn = 0; tn < NTN; ++tn) {
@@ -1060,16 +1062,21 @@ static void launch_dec_lstm(int R, const float* Wf, const ASrc& asrc, const Epi&
 template <class ASrc, class Epi>
 static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi, int s16,
                         hipStream_t s) {
-  const int nkt = KPROJ / DG_BK, NB = (ntiles + 4) / 5;
+  const int nkt = KPROJ / DG_BK, NB = (ntiles + 4) / 5;  // 5 column tiles per block (10 at R > 512)
   if (R <= 256) launch_dg<4, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  else launch_dg<8, 5, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else if (R <= 512) launch_dg<8, 5, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else launch_dg<8, 10, 2>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
 // ------------------------------------------------------------------ host drivers
 // per-block row partials from the projection epilogue: the vocabulary must fit the 64 partial
 // blocks; beam search uses them at temperature 1 only (they are of x, not x / T)
+static int proj_col_blocks(const DecodeArgs& a) {
+  const int R = a.B * a.k, nt = a.L.VP / 16;
+  return R > 512 ? (nt + 9) / 10 : (nt + 4) / 5;
+}
 static bool row_partials(const DecodeArgs& a) {
-  return (a.L.VP / 16 + 4) / 5 <= GP_NB && (a.greedy_run || a.temperature == 1.0f);
+  return proj_col_blocks(a) <= GP_NB && (a.greedy_run || a.temperature == 1.0f);
 }
 
 static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
@@ -1150,7 +1157,7 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
     if (e != hipSuccess) return e;
     ProfScope ps(a.prof, CASR_K_SELECT, s);
     if (row_partials(a)) {
-      hipLaunchKernelGGL(greedy_select_part_kernel, dim3((R + 3) / 4), dim3(256), 0, s, d.part, (a.L.VP / 16 + 4) / 5, a.V,
+      hipLaunchKernelGGL(greedy_select_part_kernel, dim3((R + 3) / 4), dim3(256), 0, s, d.part, proj_col_blocks(a), a.V,
                          R, l, a.max_len, a.eos, d.tok[(l + 1) & 1], d.src[(l + 1) & 1], finished, out_len, accum,
                          tokens, d.newdone, d.err);
     } else {
@@ -1168,7 +1175,7 @@ static void launch_beam_select(const DecodeArgs& a, DecodeBufs& d, int l, hipStr
   hipLaunchKernelGGL(kern, dim3(a.B), dim3(512), 0, s, d.logits, a.V, a.B, a.k, l,
                      a.max_len, a.eos, a.temperature, d.score[l & 1], d.score[(l + 1) & 1],
                      d.tok[(l + 1) & 1], d.src[(l + 1) & 1], d.topfin, d.bp, d.tk, d.rec_score,
-                     d.rec_src, d.rec_valid, d.newdone, d.err, d.part, row_partials(a) ? (a.L.VP / 16 + 4) / 5 : 0);
+                     d.rec_src, d.rec_valid, d.newdone, d.err, d.part, row_partials(a) ? proj_col_blocks(a) : 0);
 }
 
 hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float length_weight,
