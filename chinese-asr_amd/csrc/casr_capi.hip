@@ -805,9 +805,11 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
                                      (uint64_t)h->small.p, (uint64_t)h->bp.p, (uint64_t)h->tk.p, (uint64_t)h->rec.p,
                                      (uint64_t)h->enc_out, (uint64_t)h->keysT.p, (uint64_t)h->hfin.p,
                                      (uint64_t)h->cst.p, (uint64_t)h->lens.p};
+  dg_trace_init();  // CASR_DG_TRACE diagnostics only (outside any capture)
   HIP_OK(h, run_graph(h, key, s, [&](hipStream_t cs) {
     return run_beam(a, h->d, lm_weight, length_weight, itok, ilen, isc, istp, cs);
   }));
+  dg_trace_dump();
   HIP_OK(h, hipMemcpyAsync(best_tokens, itok, sizeof(int32_t) * B * L, hipMemcpyDeviceToDevice, s));
   HIP_OK(h, hipMemcpyAsync(best_len, ilen, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
   HIP_OK(h, hipMemcpyAsync(best_score, isc, sizeof(float) * B, hipMemcpyDeviceToDevice, s));

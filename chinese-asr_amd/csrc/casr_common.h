@@ -80,29 +80,86 @@ CASR_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 // expf/tanhf; the fast __expf differs by a few ulp, so it is not used for gates).
 CASR_DEV float sigmoid_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// ---- wave reductions on DPP lane moves (no LDS round trip; __shfl_xor lowers to ds_bpermute /
+// ds_swizzle, ~100+ cycles per dependent step).  Within each 16-lane row: quad_perm xor 1, xor 2,
+// then row_ror 4 and 8; across the 4 rows: v_readlane of lanes 0, 16, 32, 48 combined in a fixed
+// order, so every lane gets the same value (sums: row sums are read from each row's lane 0, so
+// the result does not depend on which lane computes it).  All 64 lanes must be active.
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128;
+template <int CTRL>
+CASR_DEV int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+CASR_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v)));
+}
+CASR_DEV float readlane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// every lane of each 16-lane row: that row's maximum / minimum / sum (sum: as computed in the
+// row's first quad)
+CASR_DEV float row16_max(float v) {
+  v = fmaxf(v, dpp_f<DPP_XOR1>(v));
+  v = fmaxf(v, dpp_f<DPP_XOR2>(v));
+  v = fmaxf(v, dpp_f<DPP_ROR4>(v));
+  return fmaxf(v, dpp_f<DPP_ROR8>(v));
+}
+CASR_DEV int row16_min(int v) {
+  v = min(v, dpp_i<DPP_XOR1>(v));
+  v = min(v, dpp_i<DPP_XOR2>(v));
+  v = min(v, dpp_i<DPP_ROR4>(v));
+  return min(v, dpp_i<DPP_ROR8>(v));
+}
+CASR_DEV float row16_sum(float v) {
+  v += dpp_f<DPP_XOR1>(v);
+  v += dpp_f<DPP_XOR2>(v);
+  v += dpp_f<DPP_ROR4>(v);
+  return v + dpp_f<DPP_ROR8>(v);
+}
+CASR_DEV int row16_isum(int v) {
+  v += dpp_i<DPP_XOR1>(v);
+  v += dpp_i<DPP_XOR2>(v);
+  v += dpp_i<DPP_ROR4>(v);
+  return v + dpp_i<DPP_ROR8>(v);
+}
+
+CASR_DEV float wave_max(float v) {
+  v = row16_max(v);
+  return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
+}
+
+CASR_DEV float wave_sum(float v) {
+  v = row16_sum(v);
+  return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
+}
+
+CASR_DEV int wave_min_i(int v) {
+  v = row16_min(v);
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
+// (largest value, lowest index among lanes holding it) in every lane: the `better` order of
+// the selects (greater value; on equal values the lower index)
+CASR_DEV void wave_best(float& v, int& i) {
+  const float m = wave_max(v);
+  i = wave_min_i(v == m ? i : 0x7fffffff);
+  v = m;
+}
+
 // Decode early exit (model.py:578, :897-901): newdone[s] counts rows / utterances that
 // finished at step s; step l runs only while fewer than `total` finished before it.
 // rows finished before decode step l (the per-step counters of steps 0..l-1): one wave-wide
-// load per 64 steps and a shuffle reduction, not l dependent loads
+// load per 64 steps and a DPP reduction, not l dependent loads
 CASR_DEV int done_before(const int32_t* __restrict__ newdone, int l) {
   const int lane = threadIdx.x & 63;
   int s = 0;
   for (int i0 = 0; i0 < l; i0 += 64) s += (i0 + lane < l) ? newdone[i0 + lane] : 0;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-  return s;
-}
-
-CASR_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-CASR_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  s = row16_isum(s);
+  return (__builtin_amdgcn_readlane(s, 0) + __builtin_amdgcn_readlane(s, 16)) +
+         (__builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48));
 }
 
 // Hardware-exp forms (v_exp_f32 / v_rcp_f32): the exp2 argument rounding gives exp a relative

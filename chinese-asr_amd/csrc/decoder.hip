@@ -468,14 +468,10 @@ struct ProjEpi {
           mi = n;
         }
       }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        const float om = __shfl_xor(m, o, 64);
-        const int oi = __shfl_xor(mi, o, 64);
-        if (om > m || (om == m && oi < mi)) {
-          m = om;
-          mi = oi;
-        }
+      {  // the row's (max, lowest column among equal maxima) over the 16 lanes of this g
+        const float rm = row16_max(m);
+        mi = row16_min(m == rm ? mi : 0x7fffffff);
+        m = rm;
       }
       float sx = 0.f;
 #pragma unroll
@@ -483,8 +479,7 @@ struct ProjEpi {
         const int n = (nb * NTN + tn) * 16 + u;
         if (n < V) sx += expf(x[tn] - m);
       }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) sx += __shfl_xor(sx, o, 64);
+      sx = row16_sum(sx);  // lane u == 0 (the row's first quad) writes it
       const int row = row0 + e;
       if (u == 0 && row < R) {
         gp.mx[(size_t)row * GP_NB + nb] = m;
@@ -565,15 +560,7 @@ __global__ __launch_bounds__(256) void greedy_select_kernel(
       }
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(m, o, 64);
-    const int oi = __shfl_xor(mi, o, 64);
-    if (better(ov, oi, m, mi)) {
-      m = ov;
-      mi = oi;
-    }
-  }
+  wave_best(m, mi);
   if (ln == 0) {
     sv[wv] = m;
     si[wv] = mi;
@@ -651,18 +638,8 @@ __global__ __launch_bounds__(256) void greedy_select_part_kernel(
   }
   float gm = m;
   int gi = mi;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const float om = __shfl_xor(gm, o, 64);
-    const int oi = __shfl_xor(gi, o, 64);
-    if (better(om, oi, gm, gi)) {
-      gm = om;
-      gi = oi;
-    }
-  }
-  float s = (se > 0.f) ? se * expf(m - gm) : 0.f;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  wave_best(gm, gi);
+  const float s = wave_sum((se > 0.f) ? se * expf(m - gm) : 0.f);
   if (ln != 0) return;
   const float lse = logf(s) + gm;
   const float lp = gm - lse;
@@ -735,15 +712,7 @@ __device__ __forceinline__ void wave_merge(TopList<K2>& L, int n, float* outv, i
   for (int c = 0; c < n; ++c) {
     float bv = L.v[0];
     int bi = L.i[0];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (better(ov, oi, bv, bi)) {
-        bv = ov;
-        bi = oi;
-      }
-    }
+    wave_best(bv, bi);
     if (L.i[0] == bi && L.v[0] == bv) L.pop();
     if ((threadIdx.x & 63) == 0) {
       outv[c] = bv;
@@ -776,6 +745,11 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
   __shared__ float cv_s[8][BS_CAP];  // per-wave threshold candidates
   __shared__ int ci_s[8][BS_CAP];
   __shared__ int cnt_s[8];
+  uint32_t* btr = g_dg_trace ? g_dg_trace + ((size_t)2 * 4096 + blockIdx.x) * 8 : nullptr;
+  auto stamp = [&](int i, uint32_t v) {
+    if (btr && threadIdx.x == 0) btr[i] = v;
+  };
+  stamp(0, (uint32_t)__builtin_amdgcn_s_memrealtime());
   if (done_before(newdone, l) >= B) return;
   const int b = blockIdx.x, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
   const int R = B * k;
@@ -799,9 +773,7 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
         sb = gp.se[(size_t)(b * k + j) * GP_NB + ln];
       }
       const float M = wave_max(mb);
-      float s = (sb > 0.f) ? sb * expf(mb - M) : 0.f;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      const float s = wave_sum((sb > 0.f) ? sb * expf(mb - M) : 0.f);
       lse = logf(s) + M;
       lt = (mb - lse) + sc;
     } else {
@@ -830,6 +802,7 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
       lse = logf(s) + m;
       lt = (lm - lse) + sc;
     }
+    if (j == 0) stamp(1, (uint32_t)__builtin_amdgcn_s_memrealtime());
     float tau = -INFINITY;
     for (int c = 0; c < n2k; ++c) {
       const float mx = wave_max(lt);
@@ -849,13 +822,25 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
       }
     };
     if (vec) {
-#pragma unroll 2
-      for (int i = ln; i < V / 4; i += 64) {
-        const float4 q = x4[i];
-        offer((xt(q.x) - lse) + sc, j * V + 4 * i);
-        offer((xt(q.y) - lse) + sc, j * V + 4 * i + 1);
-        offer((xt(q.z) - lse) + sc, j * V + 4 * i + 2);
-        offer((xt(q.w) - lse) + sc, j * V + 4 * i + 3);
+      // all of a lane's row loads in flight at once (20 float4 cover V = 5004), not two per
+      // round trip
+      constexpr int QB = 20;
+      for (int i0 = ln; i0 < V / 4; i0 += 64 * QB) {
+        float4 q[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          const int i = i0 + 64 * u;
+          q[u] = i < V / 4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          const int i = i0 + 64 * u;
+          if (i >= V / 4) break;
+          offer((xt(q[u].x) - lse) + sc, j * V + 4 * i);
+          offer((xt(q[u].y) - lse) + sc, j * V + 4 * i + 1);
+          offer((xt(q[u].z) - lse) + sc, j * V + 4 * i + 2);
+          offer((xt(q[u].w) - lse) + sc, j * V + 4 * i + 3);
+        }
       }
     } else {
       for (int v = ln; v < V; v += 64) offer((xt(x[v]) - lse) + sc, j * V + v);
@@ -863,6 +848,10 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     const int nc = cnt_s[wv];
+    if (j == 0) {
+      stamp(2, (uint32_t)__builtin_amdgcn_s_memrealtime());
+      stamp(7, (uint32_t)nc);
+    }
     TopList<K2> tl;
     tl.init();
     if (nc <= BS_CAP) {
@@ -878,7 +867,9 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     } else {
       for (int v = ln; v < V; v += 64) tl.insert((xt(x[v]) - lse) + sc, j * V + v);
     }
+    if (j == 0) stamp(3, (uint32_t)__builtin_amdgcn_s_memrealtime());
     wave_merge<K2>(tl, n2k, rv_s[j], ri_s[j]);
+    if (j == 0) stamp(4, (uint32_t)__builtin_amdgcn_s_memrealtime());
   }
   __syncthreads();
   if (wv == 0) {
@@ -888,43 +879,46 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     wave_merge<K2>(t2, n2k, cv, ci);
   }
   __syncthreads();
+  stamp(5, (uint32_t)__builtin_amdgcn_s_memrealtime());
 
-  if (tid == 0) {
-    for (int c = 0; c < n2k; ++c)
-      if ((unsigned)ci[c] >= (unsigned)(nrows * V)) {  // NaN rows leave empty list slots
-        atomicOr(err, CASR_DEV_BAD_CAND);
-        ci[c] = 0;
-      }
-    // finished hypotheses among the first k candidates (model.py:874-889)
-    for (int c = 0; c < k; ++c) {
-      const int beam = ci[c] / V, tok = ci[c] - beam * V;
+  // bookkeeping, one lane of wave 0 per ranked candidate c < 2k (the serial loops of
+  // model.py:874-909 as ballots: a non-EOS candidate's slot is its rank among the non-EOS ones,
+  // an EOS candidate's is (#non-EOS) + its rank among the EOS ones; slots >= k are dropped)
+  if (wv == 0) {
+    const int c = ln;
+    const bool inr = c < n2k;
+    int cc = inr ? ci[c] : 0;
+    const bool bad = inr && (unsigned)cc >= (unsigned)(nrows * V);  // NaN rows leave empty slots
+    if (bad) cc = 0;
+    if (__ballot(bad) && ln == 0) atomicOr(err, CASR_DEV_BAD_CAND);
+    const int beam = cc / V, tok = cc - beam * V;
+    const bool f = inr && tok == eos;
+    const float cs = inr ? cv[c] : 0.f;
+    if (c < k) {  // finished hypotheses among the first k candidates (model.py:874-889)
       const size_t ri = ((size_t)b * L + l) * k + c;
-      const bool f = tok == eos;
       rec_valid[ri] = f;
       if (f) {
-        rec_score[ri] = cv[c];
+        rec_score[ri] = cs;
         rec_src[ri] = beam;
       }
     }
-    const int tok0 = ci[0] % V;
-    if (!topfin[b] && tok0 == eos) {  // model.py:897-901
+    if (ln == 0 && !topfin[b] && tok == eos) {  // model.py:897-901 (candidate 0)
       topfin[b] = 1;
       atomicAdd(&newdone[l], 1);
     }
-    // active = first k non-EOS candidates in rank order (model.py:904-909)
-    int na = 0;
-    for (int pass = 0; pass < 2 && na < k; ++pass)
-      for (int c = 0; c < n2k && na < k; ++c) {
-        const int beam = ci[c] / V, tok = ci[c] - beam * V;
-        if ((tok == eos) != (pass == 1)) continue;
-        const int row = b * k + na;
-        tok_next[row] = tok;
-        src_next[row] = b * k + beam;
-        score_next[row] = cv[c];
-        bp[(size_t)l * R + row] = beam;
-        tk[(size_t)l * R + row] = tok;
-        ++na;
-      }
+    // active = first k non-EOS candidates in rank order, then EOS ones (model.py:904-909)
+    const unsigned long long ne = __ballot(inr && !f), eo = __ballot(f);
+    const unsigned long long below = (1ull << c) - 1ull;
+    const int slot = f ? __popcll(ne) + __popcll(eo & below) : __popcll(ne & below);
+    if (inr && slot < k) {
+      const int row = b * k + slot;
+      tok_next[row] = tok;
+      src_next[row] = b * k + beam;
+      score_next[row] = cs;
+      bp[(size_t)l * R + row] = beam;
+      tk[(size_t)l * R + row] = tok;
+    }
+    stamp(6, (uint32_t)__builtin_amdgcn_s_memrealtime());
   }
 }
 
@@ -1114,8 +1108,8 @@ static uint32_t* dg_trace_buffer() {
   static bool init = false;
   if (!init) {
     init = true;
-    if (std::getenv("CASR_DG_TRACE") && hipMalloc(&buf, 2 * 4096 * 8 * sizeof(uint32_t)) == hipSuccess) {
-      (void)hipMemset(buf, 0, 2 * 4096 * 8 * sizeof(uint32_t));
+    if (std::getenv("CASR_DG_TRACE") && hipMalloc(&buf, 3 * 4096 * 8 * sizeof(uint32_t)) == hipSuccess) {
+      (void)hipMemset(buf, 0, 3 * 4096 * 8 * sizeof(uint32_t));
       (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dg_trace), &buf, sizeof(buf));
     }
   }
@@ -1128,7 +1122,7 @@ void dg_trace_dump() {
   uint32_t* buf = dg_trace_buffer();
   const char* path = std::getenv("CASR_DG_TRACE");
   if (!buf || !path) return;
-  std::vector<uint32_t> h(2 * 4096 * 8);
+  std::vector<uint32_t> h(3 * 4096 * 8);
   (void)hipDeviceSynchronize();
   (void)hipMemcpy(h.data(), buf, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost);
   if (FILE* f = std::fopen(path, "wb")) {

@@ -26,7 +26,21 @@ feat, flen = eng.features(fb, torch.full((B,), T, dtype=torch.int32, device="cud
 eng.encode(feat, flen)
 eng.greedy()["tokens"].cpu()
 eng.greedy()["tokens"].cpu()
-raw = np.fromfile(PATH, dtype=np.uint32).reshape(2, 4096, 8).astype(np.int64)
+if os.environ.get("BEAM"):
+    eng.encode(feat[:128].contiguous(), flen[:128].contiguous())
+    eng.beam(8)["tokens"].cpu()
+    eng.beam(8)["tokens"].cpu()
+    raw = np.fromfile(PATH, dtype=np.uint32).reshape(3, 4096, 8).astype(np.int64)
+    r = raw[2]
+    r = r[r[:, 0] > 0]
+    t = (r[:, :7] - r[:, 0].min()) * 10 / 1000.0
+    names = ["lse+partials", "tau+offer", "list insert", "row merge", "block merge", "bookkeeping"]
+    print(f"beam_select: {len(r)} blocks, span {t[:, 6].max():.2f} us, candidates (wave 0) p50 {np.median(r[:, 7]):.0f} max {r[:, 7].max()}")
+    for i, n in enumerate(names):
+        v = t[:, i + 1] - t[:, i]
+        print(f"  {n:14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
+    sys.exit(0)
+raw = np.fromfile(PATH, dtype=np.uint32).reshape(3, 4096, 8).astype(np.int64)
 for cls, name in ((0, "dec_lstm"), (1, "proj")):
     r = raw[cls]
     r = r[r[:, 0] > 0]
