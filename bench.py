@@ -120,7 +120,7 @@ def main():
     ap.add_argument("--beam-steps", type=int, default=2)
     ap.add_argument("--no-beam", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=48)
+    ap.add_argument("--cpu-sample", type=int, default=640)
     ap.add_argument("--precision", default="s16x3", choices=["s16x3", "f32"],
                     help="MFMA arithmetic of the timed path (casr_set_precision)")
     ap.add_argument("--no-f32-compare", action="store_true",

@@ -12,6 +12,8 @@
 // 8 waves with all of a lane's 16 B loads of the phase in flight; partial sums are combined
 // through LDS in a fixed order (results are deterministic).  keysT is [B][A][Tq] (Tq = Tp
 // rounded up to 4) so a lane reads 4 consecutive time steps of one key row.
+#include <stdlib.h>
+
 #include "casr_common.h"
 #include "casr_internal.h"
 
@@ -21,6 +23,8 @@ constexpr int AT_THREADS = 512;
 constexpr int AT_WAVES = AT_THREADS / 64;
 constexpr int AT_NQ = HD / 16;  // query partials per row (one per 16-unit block of h)
 constexpr int AT_MAXG = 8;      // a-groups of the score phase
+constexpr int AT_CH = 20;       // keys rows in flight per score batch (apg = 19 at Tp = 266)
+constexpr int AT_APAD = A + AT_CH;  // q / v rows in LDS, zero-padded so a batch never branches
 
 __host__ __device__ constexpr int attn_tq(int Tp) { return (Tp + 3) & ~3; }
 
@@ -32,15 +36,19 @@ __host__ __device__ constexpr int attn_scratch_floats(int Tq) {
 
 template <int KPB>
 __host__ __device__ constexpr size_t attn_smem_floats(int Tp) {
-  return (size_t)KPB * A + A + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp);
+  return (size_t)KPB * AT_APAD + AT_APAD + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp);
 }
 
-// tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|), on v_exp_f32 / v_rcp_f32.  Absolute
-// error <= ~3e-7: every term of the score sum is this times |v[a]| (~0.1) and 128 terms are
-// summed, so the scores stay within ~1e-6 of the libm form (tests: alignment within 1e-5).
+// tanh(x) = 1 - 2 / (1 + exp(2x)) on v_exp_f32 / v_rcp_f32: mul, exp, add, rcp, fma (5 VALU
+// ops; the libm-style division __fdividef compiles to on gfx950 is an 11-instruction
+// div_scale / div_fmas / div_fixup sequence).  exp overflows to +inf for x > ~44 (rcp(inf) = 0,
+// tanh = 1) and underflows to 0 for x < ~-44 (tanh = -1).  Absolute error <= ~3e-7 (rcp 1 ulp
+// on r <= 1, exp 1 ulp damped by r(1 - r)): every term of the score sum is this times |v[a]|
+// (~0.1) and 128 terms are summed, so the scores stay within ~1e-6 of the libm form (tests:
+// alignment within 1e-5).
 CASR_DEV float tanh_fast(float x) {
-  const float e = __expf(-2.f * fabsf(x));
-  return copysignf(__fdividef(1.f - e, 1.f + e), x);
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);  // 2 log2(e) x
+  return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + e), 1.f);
 }
 
 // Memory-level parallelism is the design driver: one block (8 waves) per utterance and step
@@ -57,8 +65,8 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   __shared__ float wred[2][AT_WAVES][KPB];
   if (done_before(newdone, l) >= total) return;
   const int Tq = attn_tq(Tp);
-  float* qs = sm;                  // [KPB][A]
-  float* vs = qs + KPB * A;        // [A]
+  float* qs = sm;                  // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
+  float* vs = qs + KPB * AT_APAD;  // [AT_APAD], zero past A
   float* xs = vs + A;              // scratch
   float* es = xs + attn_scratch_floats<KPB>(Tq);  // [KPB][Tq]
   float* vl = es + KPB * Tq;                       // [npf][C]: value rows 0..npf-1 (LDS-DMA)
@@ -69,18 +77,20 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   const size_t row0 = (size_t)b * k + j0;
 
   // 1. q = sum of the HD/16 partials (fixed order), v -> LDS
-  for (int i = tid; i < nk * A; i += AT_THREADS) {
-    const int j = i / A, a = i - j * A;
-    const float* qp = qpart + (row0 + j) * A + a;
-    float pv[AT_NQ];
-#pragma unroll
-    for (int p = 0; p < AT_NQ; ++p) pv[p] = qp[(size_t)p * R * A];
+  for (int i = tid; i < KPB * AT_APAD; i += AT_THREADS) {
+    const int j = i / AT_APAD, a = i - j * AT_APAD;
     float q = 0.f;
+    if (j < nk && a < A) {
+      const float* qp = qpart + (row0 + j) * A + a;
+      float pv[AT_NQ];
 #pragma unroll
-    for (int p = 0; p < AT_NQ; ++p) q += pv[p];
-    qs[j * A + a] = q;
+      for (int p = 0; p < AT_NQ; ++p) pv[p] = qp[(size_t)p * R * A];
+#pragma unroll
+      for (int p = 0; p < AT_NQ; ++p) q += pv[p];
+    }
+    qs[a * KPB + j] = q;
   }
-  if (tid < A) vs[tid] = vv[tid];
+  if (tid < AT_APAD) vs[tid] = tid < A ? vv[tid] : 0.f;
   __syncthreads();
 
   // 2. scores.  Thread = (a-group ag, 4-step chunk c): its APG keys rows' float4 at chunk c are
@@ -89,7 +99,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
   const int apg = (A + G - 1) / G;
   const float* kb = keysT + (size_t)b * A * Tq;
-  constexpr int CH = 20;  // keys rows in flight per batch (apg = 19 at Tp = 266)
+  constexpr int CH = AT_CH;
   // this thread's score work: (a-group, 4-step chunk) items it = tid, tid + 512, ...; each in
   // batches of CH keys rows
   auto score_item = [&](int it, bool first, auto&& after_loads) {
@@ -99,20 +109,21 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float e4[KPB][4];
 #pragma unroll
     for (int j = 0; j < KPB; ++j) e4[j][0] = e4[j][1] = e4[j][2] = e4[j][3] = 0.f;
+    // branch-free: a slot past the group's last row gets v = 0 (its keys load is zero-filled and
+    // q is padded), so it adds an exact zero and the real terms keep their order; rows j >= nk
+    // compute on q = 0 and are never stored
     auto batch = [&](const float4 (&kv)[CH], int ab) {
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
-        if (ab + i >= a1) break;
-        const float va = vs[ab + i];
+        const float va = ab + i < a1 ? vs[ab + i] : 0.f;
 #pragma unroll
-        for (int j = 0; j < KPB; ++j)
-          if (j < nk) {
-            const float qa = qs[j * A + ab + i];
-            e4[j][0] = __fadd_rn(e4[j][0], __fmul_rn(tanh_fast(kv[i].x + qa), va));
-            e4[j][1] = __fadd_rn(e4[j][1], __fmul_rn(tanh_fast(kv[i].y + qa), va));
-            e4[j][2] = __fadd_rn(e4[j][2], __fmul_rn(tanh_fast(kv[i].z + qa), va));
-            e4[j][3] = __fadd_rn(e4[j][3], __fmul_rn(tanh_fast(kv[i].w + qa), va));
-          }
+        for (int j = 0; j < KPB; ++j) {
+          const float qa = qs[(ab + i) * KPB + j];
+          e4[j][0] = __fadd_rn(e4[j][0], __fmul_rn(tanh_fast(kv[i].x + qa), va));
+          e4[j][1] = __fadd_rn(e4[j][1], __fmul_rn(tanh_fast(kv[i].y + qa), va));
+          e4[j][2] = __fadd_rn(e4[j][2], __fmul_rn(tanh_fast(kv[i].z + qa), va));
+          e4[j][3] = __fadd_rn(e4[j][3], __fmul_rn(tanh_fast(kv[i].w + qa), va));
+        }
       }
     };
     auto load = [&](float4 (&kv)[CH], int ab) {
@@ -304,10 +315,21 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 
 // value rows prefetched into LDS by each block: what fits beside the block's other LDS (160 KiB
 // per CU, one block per CU), a multiple of 4 rows
+// CASR_ATTN_LDS_KB: LDS budget per block in KiB (tuning knob; default 156 = one block per CU)
+static size_t attn_lds_budget() {
+  static const size_t v = [] {
+    const char* e = std::getenv("CASR_ATTN_LDS_KB");
+    const int kb = e ? std::atoi(e) : 156;
+    return (size_t)(kb > 16 && kb <= 156 ? kb : 156) * 1024;
+  }();
+  return v;
+}
+
 template <int KPB>
 static int attn_npf(int Tp) {
   const size_t fixed = attn_smem_floats<KPB>(Tp) * sizeof(float) + 2 * AT_WAVES * KPB * sizeof(float);
-  const size_t room = fixed < 156 * 1024 ? 156 * 1024 - fixed : 0;
+  const size_t budget = attn_lds_budget();
+  const size_t room = fixed < budget ? budget - fixed : 0;
   const int rows = (int)(room / (C * sizeof(float))) & ~3;
   return rows < Tp ? rows : (Tp + 3) & ~3;
 }
@@ -335,7 +357,13 @@ hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qp
   if (a.k == 1) return launch_kpb<1>(a, st, qpart, align, newdone, l, total, s);
   if (a.k == 2) return launch_kpb<2>(a, st, qpart, align, newdone, l, total, s);
   // k > 4 keeps 4 rows per block: 8 rows per block (one block per utterance, half the grid)
-  // measured 3.68 ms vs 2.87 ms per B = 128, k = 8 batch
+  // measured 3.68 ms vs 2.87 ms per B = 128, k = 8 batch.  CASR_ATTN_KPB = 1 or 2: tuning knob
+  static const int kpb = [] {
+    const char* e = std::getenv("CASR_ATTN_KPB");
+    return e ? std::atoi(e) : 4;
+  }();
+  if (kpb == 1) return launch_kpb<1>(a, st, qpart, align, newdone, l, total, s);
+  if (kpb == 2) return launch_kpb<2>(a, st, qpart, align, newdone, l, total, s);
   return launch_kpb<4>(a, st, qpart, align, newdone, l, total, s);
 }
 
