@@ -162,14 +162,18 @@ CASR_DEV int done_before(const int32_t* __restrict__ newdone, int l) {
          (__builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48));
 }
 
-// Hardware-exp forms (v_exp_f32 / v_rcp_f32): the exp2 argument rounding gives exp a relative
-// error ~|x| 6e-8, which the sigmoid's slope damps (absolute error <~1e-8); tanh = (1-e)/(1+e),
-// e = exp(-2|x|), has absolute error ~1e-7.  Used by the encoder cell in s16x3 arithmetic (the
-// f32 arithmetic keeps the libm cell below).
-CASR_DEV float sigmoid_hw(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+// Hardware-exp forms (v_exp_f32 / v_rcp_f32, no IEEE division: __frcp_rn / __fdividef / 1.f / x
+// compile to a div_scale / div_fmas / div_fixup sequence of ~10 dependent instructions, and this
+// cell sits on the recurrence's critical path).  exp(y) = exp2(y log2 e) with the product rounded
+// once: relative error ~|y| 6e-8, which the sigmoid's slope damps (absolute error <~1e-8); v_rcp_f32
+// is within 1 ulp.  tanh = sign(x) (1 - e) / (1 + e), e = exp(-2|x|): absolute error ~2e-7.  Used by
+// the encoder cell in s16x3 arithmetic (the f32 arithmetic keeps the libm cell below).
+CASR_DEV float sigmoid_hw(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
 CASR_DEV float tanh_hw(float x) {
-  const float e = __expf(-2.f * fabsf(x));
-  return copysignf(__fdividef(1.f - e, 1.f + e), x);
+  const float e = __builtin_amdgcn_exp2f(fabsf(x) * -2.8853900817779268f);
+  return copysignf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e), x);
 }
 CASR_DEV void lstm_cell_hw(float gi, float gf, float gg, float go, float c, float& h2, float& c2) {
   const float i = sigmoid_hw(gi), f = sigmoid_hw(gf), g = tanh_hw(gg), o = sigmoid_hw(go);
