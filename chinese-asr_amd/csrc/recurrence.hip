@@ -141,7 +141,9 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   // epilogue operands that do not depend on h (Gin gates, residual input) are software-pipelined
   // one step ahead: step s+1's are issued right after step s's granule sweep, so they land
   // during the MFMAs / cell instead of in front of the next sweep's vmcnt(0) wait
-  float gin_v[4] = {0.f, 0.f, 0.f, 0.f}, x_res = 0.f;
+  // gin_n / x_n: the operands of the next step to run, in flight; copied to gin_v / x_res right after
+  // a step's sweep, whose vmcnt(0) has retired them (so the copy never waits)
+  float gin_n[4] = {0.f, 0.f, 0.f, 0.f}, x_n = 0.f;
   auto load_operands = [&](int s, float (&g)[4], float& xr) {
     if (s < len) {
       const int t = (d == 0) ? s : (len - 1 - s);
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       if (residual) xr = xin[((size_t)b * Tp + t) * C + d * H + U];
     }
   };
-  load_operands(0, gin_v, x_res);
+  load_operands(0, gin_n, x_n);
   uint32_t* tr = trace ? trace + ((size_t)(grp * P + mem) * NW + w) * Tp * 5 : nullptr;
   for (int s = 0; s < tmax; ++s) {
     const bool act = s < len;
@@ -160,23 +162,24 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     f32x4 acc[4];
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) acc[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float gin_n[4] = {0.f, 0.f, 0.f, 0.f}, x_n = 0.f;
+    u32x4 v[4];
     if (s > 0) {
       // h_{s-1}: words tagged with the parity of s in buffer s % 3
       uint32_t* src = hx + (size_t)(s % 3) * 2 * plane + wbase;
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc(src, 0, 16 * H * (int)sizeof(uint32_t), 0x00020000);
       const uint32_t want = (s & 1) ? TAG_BIT : 0u;
-      u32x4 v[4];
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (uint32_t pass = 0;; ++pass) {
         asm volatile("" ::: "memory");
         uint32_t bad = 0;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + i * 16, 0, 16 /* sc1 */);
-          bad |= (v[i].x ^ want) | (v[i].y ^ want) | (v[i].z ^ want) | (v[i].w ^ want);
-        }
+        for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + i * 16, 0, 16 /* sc1 */);
+        // all four loads in flight before any check (hipcc otherwise may interleave load / wait /
+        // check: four round trips per pass)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bad |= (v[i].x ^ want) | (v[i].y ^ want) | (v[i].z ^ want) | (v[i].w ^ want);
         const bool ok = (bad & TAG_BIT) == 0;
         npass = pass + 1;
         if (__all(ok)) break;
@@ -191,7 +194,16 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
         __builtin_amdgcn_s_sleep(1);
       }
       if (tr && lane == 0) tr[s * 5 + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
-      load_operands(s + 1, gin_n, x_n);
+    }
+    // this step's operands (landed: retired by the sweep's vmcnt(0), or on entry), then the next
+    // step's loads, which land under the MFMAs / cell.  The copy sits here and not at the loop
+    // end, where it waited for loads issued only ~1 us earlier
+    float gin_v[4], x_res;
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) gin_v[tn] = gin_n[tn];
+    x_res = x_n;
+    load_operands(s + 1, gin_n, x_n);
+    if (s > 0) {
       if constexpr (S16) {
         f32x4 accx[4];
 #pragma unroll
@@ -223,8 +235,6 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
           }
         }
       }
-    } else {
-      load_operands(1, gin_n, x_n);
     }
     f32x4 (*rb)[4][64] = red[s & 1];
 #pragma unroll
@@ -262,9 +272,6 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       tr[s * 5 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
       tr[s * 5 + 4] = npass;
     }
-#pragma unroll
-    for (int tn = 0; tn < 4; ++tn) gin_v[tn] = gin_n[tn];
-    x_res = x_n;
   }
   if (b < B) cst[si] = c;
 }
