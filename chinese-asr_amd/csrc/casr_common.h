@@ -74,6 +74,20 @@ CASR_DEV void mfma_s16(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x4& hh, f32x4&
 
 CASR_DEV float s16_combine(float hh, float x) { return hh + x * S16_LO_INV; }
 
+// global_load_lds_dwordx4 in inline asm: hipcc does not see these DMAs, so it inserts no wait of
+// its own for them (seen, every ds_read of the ring waited vmcnt(0): the DMAs carry no alias
+// scope); the kernel orders them itself with counted vmcnt waits + s_barrier.  M0 = the wave's
+// LDS destination base (lane l writes base + 16 l), saved and restored around the load.
+CASR_DEV void lds_dma16(const float* src, float* lds_wave_base) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds_wave_base);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+
 CASR_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // Accurate variants used on every parity-relevant path (torch CPU uses libm-accurate

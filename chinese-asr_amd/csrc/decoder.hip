@@ -66,19 +66,7 @@ __device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
 
 inline unsigned xcd_grid(int NB, int NR) { return (unsigned)(8 * ((NB + 7) / 8) * NR); }
 
-// global_load_lds_dwordx4 in inline asm: hipcc does not see these DMAs, so it inserts no wait of
-// its own for them (seen, every ds_read of the ring waited vmcnt(0): the DMAs carry no alias
-// scope); the kernel orders them itself with counted vmcnt waits + s_barrier.  M0 = the wave's
-// LDS destination base (lane l writes base + 16 l), saved and restored around the load.
-__device__ __forceinline__ void lds_dma16(const float* src, float* lds_wave_base) {
-  const uint32_t lds = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds_wave_base);
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(lds)
-               : "memory");
-}
+// lds_dma16 (casr_common.h): global_load_lds_dwordx4 from inline asm
 
 // s_waitcnt vmcnt(N) alone (gfx9 encoding: vmcnt[3:0], expcnt 7, lgkmcnt 15, vmcnt[5:4] << 14)
 template <int N>
