@@ -82,7 +82,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
-    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg) {
+    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg, int pre_wait, int pre_sleep) {
   constexpr int NW = RG * UW / 64;      // waves: 4 k-chunks x RG/16 row halves x UW/16 unit halves
   __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
@@ -141,9 +141,6 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   // epilogue operands that do not depend on h (Gin gates, residual input) are software-pipelined
   // one step ahead: step s+1's are issued right after step s's granule sweep, so they land
   // during the MFMAs / cell instead of in front of the next sweep's vmcnt(0) wait
-  // gin_n / x_n: the operands of the next step to run, in flight; copied to gin_v / x_res right after
-  // a step's sweep, whose vmcnt(0) has retired them (so the copy never waits)
-  float gin_n[4] = {0.f, 0.f, 0.f, 0.f}, x_n = 0.f;
   auto load_operands = [&](int s, float (&g)[4], float& xr) {
     if (s < len) {
       const int t = (d == 0) ? s : (len - 1 - s);
@@ -153,9 +150,17 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       if (residual) xr = xin[((size_t)b * Tp + t) * C + d * H + U];
     }
   };
-  load_operands(0, gin_n, x_n);
   uint32_t* tr = trace ? trace + ((size_t)(grp * P + mem) * NW + w) * Tp * 5 : nullptr;
-  for (int s = 0; s < tmax; ++s) {
+  // The loop runs two steps per iteration over two statically named operand sets (A, B): step s
+  // uses the set loaded after sweep s-1 (retired by sweep s's vmcnt(0)) and loads the other one
+  // for s+1 right after its own sweep, so no operand register is copied and nothing waits at the
+  // loop latch (a one-set loop copied the fresh loads there behind a vmcnt(0) that also waited
+  // for the step's stores).
+  // FIRST (step 0, peeled): no sweep, no MFMA.  The later steps have both unconditionally, so every
+  // operand load is provably retired by the sweep's vmcnt(0) before its use.
+  auto step = [&](auto first_c, const int s, const float (&gin_v)[4], const float x_res, float (&gin_n)[4],
+                  float& x_n) -> bool {
+    constexpr bool FIRST = decltype(first_c)::value;
     const bool act = s < len;
     uint32_t npass = 0;
     if (tr && lane == 0) tr[s * 5 + 0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -163,12 +168,19 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) acc[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
     u32x4 v[4];
-    if (s > 0) {
+    if constexpr (!FIRST) {
       // h_{s-1}: words tagged with the parity of s in buffer s % 3
       uint32_t* src = hx + (size_t)(s % 3) * 2 * plane + wbase;
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc(src, 0, 16 * H * (int)sizeof(uint32_t), 0x00020000);
       const uint32_t want = (s & 1) ? TAG_BIT : 0u;
+      // pacing of the first poll (CASR_REC_PREWAIT / CASR_REC_PRESLEEP, tuning knobs): wait for
+      // this wave's own stores of the previous step (vmcnt(0)), then sleep pre_sleep x 64 clocks.
+      // A poll issued before the group's stores have landed fails and costs a whole extra round
+      // trip.  Measured (ms per greedy batch): no wait 5.95, wait + sleep 0 / 2 / 4 / 5 / 6 / 8 /
+      // 10 = 3.05 / 3.24 / 2.91 / 2.80 / 2.82-2.85 / 2.87 / 2.89; default wait + 6.
+      if (pre_wait) __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
+      for (int i = 0; i < pre_sleep; ++i) __builtin_amdgcn_s_sleep(1);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (uint32_t pass = 0;; ++pass) {
         asm volatile("" ::: "memory");
@@ -195,15 +207,8 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       }
       if (tr && lane == 0) tr[s * 5 + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
-    // this step's operands (landed: retired by the sweep's vmcnt(0), or on entry), then the next
-    // step's loads, which land under the MFMAs / cell.  The copy sits here and not at the loop
-    // end, where it waited for loads issued only ~1 us earlier
-    float gin_v[4], x_res;
-#pragma unroll
-    for (int tn = 0; tn < 4; ++tn) gin_v[tn] = gin_n[tn];
-    x_res = x_n;
     load_operands(s + 1, gin_n, x_n);
-    if (s > 0) {
+    if constexpr (!FIRST) {
       if constexpr (S16) {
         f32x4 accx[4];
 #pragma unroll
@@ -240,7 +245,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) rb[w][tn][lane] = acc[tn];
     __syncthreads();
-    if (s_quit[s & 1]) break;
+    if (s_quit[s & 1]) return false;
     if (tr && lane == 0) tr[s * 5 + 2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 
     // cell (same reduction order as rec_step_kernel: k-chunks 0..3, then + Gin)
@@ -272,6 +277,15 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       tr[s * 5 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
       tr[s * 5 + 4] = npass;
     }
+    return true;
+  };
+  float gA[4] = {0.f, 0.f, 0.f, 0.f}, gB[4] = {0.f, 0.f, 0.f, 0.f}, xA = 0.f, xB = 0.f;
+  load_operands(0, gA, xA);
+  if (tmax > 0 && step(std::true_type{}, 0, gA, xA, gB, xB)) {
+    for (int s = 1; s < tmax; s += 2) {
+      if (!step(std::false_type{}, s, gB, xB, gA, xA)) break;
+      if (s + 1 < tmax && !step(std::false_type{}, s + 1, gA, xA, gB, xB)) break;
+    }
   }
   if (b < B) cst[si] = c;
 }
@@ -279,6 +293,19 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
 }  // namespace
 
 // CASR_REC_LAYOUT = rows x units per workgroup: 32x16 (default), 16x32 or 16x16 (tuning knob)
+static int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+static int rec_pre_wait() {
+  static const int v = env_int("CASR_REC_PREWAIT", 1);
+  return v;
+}
+static int rec_pre_sleep() {
+  static const int v = env_int("CASR_REC_PRESLEEP", 6);
+  return v;
+}
+
 static int rec_layout() {
   static const int v = [] {
     const char* e = std::getenv("CASR_REC_LAYOUT");
@@ -337,7 +364,7 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
   dim3 grid((H / UW) * nrg * 2);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(RG * UW), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens, B, Bp, Tp,
-                       residual, err, trace, nrg);
+                       residual, err, trace, nrg, rec_pre_wait(), rec_pre_sleep());
   };
   switch (rec_layout()) {
     case 1: s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>); break;
