@@ -56,6 +56,9 @@ CASR_DEV float tanh_fast(float x) {
 // of a lane's loads of that phase in flight at once (one round trip per phase, not one per
 // unrolled batch).  The query q = h . W_hidden arrives as HD/16 partials written by the decoder
 // LSTM epilogue (decoder.hip DecLstmEpi), so W_hidden is not re-read per block.
+// diagnostics (CASR_DG_TRACE, tools/probes/dg_trace.py): per-block phase stamps of the last launch
+__device__ uint32_t* g_at_trace = nullptr;
+
 template <int KPB>
 __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float* __restrict__ st, const float* __restrict__ qpart, const float* __restrict__ keysT,
@@ -63,12 +66,17 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l, int total, int npf) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ float wred[2][AT_WAVES][KPB];
+  uint32_t* atr = g_at_trace ? g_at_trace + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
+  auto stamp = [&](int i) {
+    if (atr && threadIdx.x == 0) atr[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   if (done_before(newdone, l) >= total) return;
   const int Tq = attn_tq(Tp);
   float* qs = sm;                  // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
   float* vs = qs + KPB * AT_APAD;  // [AT_APAD], zero past A
   float* xs = vs + A;              // scratch
-  float* es = xs + attn_scratch_floats<KPB>(Tq);  // [KPB][Tq]
+  float* es = xs + attn_scratch_floats<KPB>(Tq);  // [Tq][KPB]: one 4 x KPB-byte read per t
   float* vl = es + KPB * Tq;                       // [npf][C]: value rows 0..npf-1 (LDS-DMA)
   const int b = blockIdx.x, j0 = blockIdx.y * KPB;
   const int nk = min(KPB, k - j0);
@@ -92,6 +100,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   }
   if (tid < AT_APAD) vs[tid] = tid < A ? vv[tid] : 0.f;
   __syncthreads();
+  stamp(1);
 
   // 2. scores.  Thread = (a-group ag, 4-step chunk c): its APG keys rows' float4 at chunk c are
   // all loaded before use; partial sums per a-group go to LDS and are added in group order.
@@ -171,6 +180,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   });
   for (int it = tid + AT_THREADS; it < G * nch; it += AT_THREADS) score_item(it, false, [] {});
   __syncthreads();
+  stamp(2);
 
   // combine the G group partials (fixed order), mask past len, row maxima
   float lmax[KPB];
@@ -186,7 +196,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
           ev = x[0];
           for (int gg = 1; gg < G; ++gg) ev += x[gg * gs];
         }
-        es[j * Tq + t] = ev;
+        es[t * KPB + j] = ev;
         lmax[j] = fmaxf(lmax[j], ev);
       }
   }
@@ -212,8 +222,8 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   for (int j = 0; j < KPB; ++j)
     if (j < nk)
       for (int t = tid; t < Tq; t += AT_THREADS) {
-        const float p = expf(es[j * Tq + t] - rmax[j]);
-        es[j * Tq + t] = p;
+        const float p = expf(es[t * KPB + j] - rmax[j]);
+        es[t * KPB + j] = p;
         lsum[j] += p;
       }
 #pragma unroll
@@ -237,8 +247,8 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   for (int j = 0; j < KPB; ++j)
     if (j < nk)
       for (int t = tid; t < Tq; t += AT_THREADS) {
-        const float al = es[j * Tq + t] * rinv[j];
-        es[j * Tq + t] = al;
+        const float al = es[t * KPB + j] * rinv[j];
+        es[t * KPB + j] = al;
         if (align && t < Tp) align[(size_t)t * RR + row0 + j] = al;
       }
   __syncthreads();
@@ -255,18 +265,35 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     // each thread's t sequence continues unchanged into the global rows: same summation order)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    stamp(3);
+    // alpha of the KPB rows at step t: one LDS read ([Tq][KPB] layout); t is clamped to Tq - 1,
+    // which only slots past len reach, and their value rows are zero-filled, so they add exact zeros
+    // (alpha is finite everywhere: 0 past len) and the loop needs no exit test per t
+    auto alpha = [&](int t, float (&al)[KPB]) {
+      const float* ep = es + min(t, Tq - 1) * KPB;
+      if constexpr (KPB == 4) {
+        const float4 a4 = *reinterpret_cast<const float4*>(ep);
+        al[0] = a4.x, al[1] = a4.y, al[2] = a4.z, al[3] = a4.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < KPB; ++j) al[j] = ep[j];
+      }
+    };
+    auto fma4 = [&](const float (&al)[KPB], const float4& v) {
+#pragma unroll
+      for (int j = 0; j < KPB; ++j) {
+        acc[j][0] = __fadd_rn(acc[j][0], __fmul_rn(al[j], v.x));
+        acc[j][1] = __fadd_rn(acc[j][1], __fmul_rn(al[j], v.y));
+        acc[j][2] = __fadd_rn(acc[j][2], __fmul_rn(al[j], v.z));
+        acc[j][3] = __fadd_rn(acc[j][3], __fmul_rn(al[j], v.w));
+      }
+    };
     int t = tp;
     for (; t < nv; t += 4) {
       const float4 v = *reinterpret_cast<const float4*>(vl + (size_t)t * C + 4 * c4);
-#pragma unroll
-      for (int j = 0; j < KPB; ++j)
-        if (j < nk) {
-          const float al = es[j * Tq + t];
-          acc[j][0] = __fadd_rn(acc[j][0], __fmul_rn(al, v.x));
-          acc[j][1] = __fadd_rn(acc[j][1], __fmul_rn(al, v.y));
-          acc[j][2] = __fadd_rn(acc[j][2], __fmul_rn(al, v.z));
-          acc[j][3] = __fadd_rn(acc[j][3], __fmul_rn(al, v.w));
-        }
+      float al[KPB];
+      alpha(t, al);
+      fma4(al, v);
     }
     constexpr int CT = 32;
     for (int tb = t; tb < len; tb += 4 * CT) {
@@ -278,17 +305,9 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       }
 #pragma unroll
       for (int i = 0; i < CT; ++i) {
-        const int t = tb + 4 * i;
-        if (t >= len) break;
-#pragma unroll
-        for (int j = 0; j < KPB; ++j)
-          if (j < nk) {
-            const float al = es[j * Tq + t];
-            acc[j][0] = __fadd_rn(acc[j][0], __fmul_rn(al, v4[i].x));
-            acc[j][1] = __fadd_rn(acc[j][1], __fmul_rn(al, v4[i].y));
-            acc[j][2] = __fadd_rn(acc[j][2], __fmul_rn(al, v4[i].z));
-            acc[j][3] = __fadd_rn(acc[j][3], __fmul_rn(al, v4[i].w));
-          }
+        float al[KPB];
+        alpha(tb + 4 * i, al);
+        fma4(al, v4[i]);
       }
     }
 #pragma unroll
@@ -297,6 +316,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
         *reinterpret_cast<float4*>(xs + (tp * KPB + j) * C + 4 * c4) =
             make_float4(acc[j][0], acc[j][1], acc[j][2], acc[j][3]);
   }
+  stamp(4);
   __syncthreads();
   for (int i = tid; i < nk * (C / 4); i += AT_THREADS) {
     const int j = i / (C / 4), c4 = i - j * (C / 4);
@@ -311,6 +331,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     *reinterpret_cast<u32x4*>(st + (row0 + j) * ST + ST16 + 4 * c4) =
         u32x4{split16_word(cv.x), split16_word(cv.y), split16_word(cv.z), split16_word(cv.w)};
   }
+  stamp(5);
 }
 
 // value rows prefetched into LDS by each block: what fits beside the block's other LDS (160 KiB
@@ -371,5 +392,7 @@ size_t attention_smem_bytes(int k, int Tp) {
   const size_t f = k == 1 ? attn_smem_floats<1>(Tp) : k == 2 ? attn_smem_floats<2>(Tp) : attn_smem_floats<4>(Tp);
   return f * sizeof(float);
 }
+
+void attn_trace_bind(uint32_t* buf) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_at_trace), &buf, sizeof(buf)); }
 
 }  // namespace casr

@@ -251,6 +251,7 @@ struct DecodeArgs {
 hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
                                  int32_t* newdone, int l, int total, hipStream_t s);
 size_t attention_smem_bytes(int k, int Tp);
+void attn_trace_bind(uint32_t* buf);  // CASR_DG_TRACE diagnostics (attention.hip)
 
 void dg_trace_init();  // decoder.hip, CASR_DG_TRACE diagnostics
 void dg_trace_dump();

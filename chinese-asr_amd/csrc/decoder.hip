@@ -1096,9 +1096,10 @@ static uint32_t* dg_trace_buffer() {
   static bool init = false;
   if (!init) {
     init = true;
-    if (std::getenv("CASR_DG_TRACE") && hipMalloc(&buf, 3 * 4096 * 8 * sizeof(uint32_t)) == hipSuccess) {
-      (void)hipMemset(buf, 0, 3 * 4096 * 8 * sizeof(uint32_t));
+    if (std::getenv("CASR_DG_TRACE") && hipMalloc(&buf, 4 * 4096 * 8 * sizeof(uint32_t)) == hipSuccess) {
+      (void)hipMemset(buf, 0, 4 * 4096 * 8 * sizeof(uint32_t));
       (void)hipMemcpyToSymbol(HIP_SYMBOL(g_dg_trace), &buf, sizeof(buf));
+      attn_trace_bind(buf + 3 * 4096 * 8);  // class 3: attention (attention.hip)
     }
   }
   return buf;
@@ -1110,7 +1111,7 @@ void dg_trace_dump() {
   uint32_t* buf = dg_trace_buffer();
   const char* path = std::getenv("CASR_DG_TRACE");
   if (!buf || !path) return;
-  std::vector<uint32_t> h(3 * 4096 * 8);
+  std::vector<uint32_t> h(4 * 4096 * 8);
   (void)hipDeviceSynchronize();
   (void)hipMemcpy(h.data(), buf, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost);
   if (FILE* f = std::fopen(path, "wb")) {

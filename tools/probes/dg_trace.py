@@ -18,6 +18,17 @@ from casr.engine import Engine  # noqa: E402
 from casr.weights import synthetic_state_dicts  # noqa: E402
 
 B, T = int(os.environ.get("B", 256)), 800
+
+
+def attn_report(r, title):
+    r = r[r[:, 0] > 0]
+    t = (r[:, :6] - r[:, 0].min()) * 10 / 1000.0
+    print(f"{title}: {len(r)} blocks, span {t[:, 5].max():.2f} us")
+    for i, n in enumerate(["q partials", "scores", "softmax", "context", "reduce+store"]):
+        v = t[:, i + 1] - t[:, i]
+        print(f"  {n:14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
+    v = t[:, 0]
+    print(f"  {'start':14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
 cfg = CasrConfig()
 eng = Engine(cfg, *synthetic_state_dicts(cfg, peaked=True, eos_bias=0.0))
 fb = torch.from_numpy(np.stack([np.random.RandomState(1234 + b).standard_normal((T, 80)).astype(np.float32)
@@ -30,17 +41,19 @@ if os.environ.get("BEAM"):
     eng.encode(feat[:128].contiguous(), flen[:128].contiguous())
     eng.beam(8)["tokens"].cpu()
     eng.beam(8)["tokens"].cpu()
-    raw = np.fromfile(PATH, dtype=np.uint32).reshape(3, 4096, 8).astype(np.int64)
+    raw = np.fromfile(PATH, dtype=np.uint32).reshape(4, 4096, 8).astype(np.int64)
     r = raw[2]
     r = r[r[:, 0] > 0]
     t = (r[:, :7] - r[:, 0].min()) * 10 / 1000.0
+    attn_report(raw[3], "attention (beam)")
     names = ["lse+partials", "tau+offer", "list insert", "row merge", "block merge", "bookkeeping"]
     print(f"beam_select: {len(r)} blocks, span {t[:, 6].max():.2f} us, candidates (wave 0) p50 {np.median(r[:, 7]):.0f} max {r[:, 7].max()}")
     for i, n in enumerate(names):
         v = t[:, i + 1] - t[:, i]
         print(f"  {n:14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
     sys.exit(0)
-raw = np.fromfile(PATH, dtype=np.uint32).reshape(3, 4096, 8).astype(np.int64)
+raw = np.fromfile(PATH, dtype=np.uint32).reshape(4, 4096, 8).astype(np.int64)
+attn_report(raw[3], "attention (greedy)")
 for cls, name in ((0, "dec_lstm"), (1, "proj")):
     r = raw[cls]
     r = r[r[:, 0] > 0]
