@@ -85,10 +85,12 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   const size_t row0 = (size_t)b * k + j0;
 
   // 1. q = sum of the HD/16 partials (fixed order), v -> LDS
-  for (int i = tid; i < KPB * AT_APAD; i += AT_THREADS) {
-    const int j = i / AT_APAD, a = i - j * AT_APAD;
+  // (KPB x A = 128 KPB items: one round of 16 loads per thread at KPB <= 4; the zero pad rows
+  // a >= A take no loads)
+  for (int i = tid; i < KPB * A; i += AT_THREADS) {
+    const int j = i / A, a = i - j * A;
     float q = 0.f;
-    if (j < nk && a < A) {
+    if (j < nk) {
       const float* qp = qpart + (row0 + j) * A + a;
       float pv[AT_NQ];
 #pragma unroll
@@ -98,6 +100,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     }
     qs[a * KPB + j] = q;
   }
+  for (int i = tid; i < KPB * (AT_APAD - A); i += AT_THREADS) qs[A * KPB + i] = 0.f;
   if (tid < AT_APAD) vs[tid] = tid < A ? vv[tid] : 0.f;
   __syncthreads();
   stamp(1);
