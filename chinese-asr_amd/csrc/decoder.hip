@@ -840,24 +840,49 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
       stamp(2, (uint32_t)__builtin_amdgcn_s_memrealtime());
       stamp(7, (uint32_t)nc);
     }
-    TopList<K2> tl;
-    tl.init();
     if (nc <= BS_CAP) {
-      for (int p = ln; p < nc; p += 64) tl.insert(cv_s[wv][p], ci_s[wv][p]);
-    } else if (vec) {  // more ties at tau than the buffer holds: every element
-      for (int i = ln; i < V / 4; i += 64) {
-        const float4 q = x4[i];
-        tl.insert((xt(q.x) - lse) + sc, j * V + 4 * i);  // model.py:834-836
-        tl.insert((xt(q.y) - lse) + sc, j * V + 4 * i + 1);
-        tl.insert((xt(q.z) - lse) + sc, j * V + 4 * i + 2);
-        tl.insert((xt(q.w) - lse) + sc, j * V + 4 * i + 3);
+      // rank selection over the row's threshold candidates (a few dozen): a candidate's slot is
+      // the number of candidates better than it (better(): value, then lower flat index; indices
+      // are distinct, so ranks are too); slots no candidate reaches keep the (-inf, INT_MAX)
+      // sentinel the sorted-list merge (wave_merge) produces for them.  Same list, in sorted
+      // order, as the per-lane insertion + wave_merge below, without its 2k shuffle rounds.
+      if (ln < n2k) {
+        rv_s[j][ln] = -INFINITY;
+        ri_s[j][ln] = 0x7fffffff;
       }
-    } else {
-      for (int v = ln; v < V; v += 64) tl.insert((xt(x[v]) - lse) + sc, j * V + v);
+      __builtin_amdgcn_wave_barrier();
+      for (int p = ln; p < nc; p += 64) {
+        const float pv = cv_s[wv][p];
+        const int pi = ci_s[wv][p];
+        int rank = 0;
+        for (int q = 0; q < nc; ++q) rank += better(cv_s[wv][q], ci_s[wv][q], pv, pi) ? 1 : 0;
+        if (rank < n2k) {
+          rv_s[j][rank] = pv;
+          ri_s[j][rank] = pi;
+        }
+      }
+      if (j == 0) {
+        stamp(3, (uint32_t)__builtin_amdgcn_s_memrealtime());
+        stamp(4, (uint32_t)__builtin_amdgcn_s_memrealtime());
+      }
+    } else {  // more ties at tau than the buffer holds: every element through sorted lane lists
+      TopList<K2> tl;
+      tl.init();
+      if (vec) {
+        for (int i = ln; i < V / 4; i += 64) {
+          const float4 q = x4[i];
+          tl.insert((xt(q.x) - lse) + sc, j * V + 4 * i);  // model.py:834-836
+          tl.insert((xt(q.y) - lse) + sc, j * V + 4 * i + 1);
+          tl.insert((xt(q.z) - lse) + sc, j * V + 4 * i + 2);
+          tl.insert((xt(q.w) - lse) + sc, j * V + 4 * i + 3);
+        }
+      } else {
+        for (int v = ln; v < V; v += 64) tl.insert((xt(x[v]) - lse) + sc, j * V + v);
+      }
+      if (j == 0) stamp(3, (uint32_t)__builtin_amdgcn_s_memrealtime());
+      wave_merge<K2>(tl, n2k, rv_s[j], ri_s[j]);
+      if (j == 0) stamp(4, (uint32_t)__builtin_amdgcn_s_memrealtime());
     }
-    if (j == 0) stamp(3, (uint32_t)__builtin_amdgcn_s_memrealtime());
-    wave_merge<K2>(tl, n2k, rv_s[j], ri_s[j]);
-    if (j == 0) stamp(4, (uint32_t)__builtin_amdgcn_s_memrealtime());
   }
   __syncthreads();
   if (wv == 0) {
