@@ -541,6 +541,10 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   float* outs[2] = {h->out0.as<float>(), h->out1.as<float>()};
   const float* x = feat;
   float* hb = h->hbuf.as<float>();
+  // s16: a persistent layer writes the next layer's input row image itself (no split pass);
+  // CASR_FUSE_SPLIT=0 restores the separate split_rows pass (A/B knob)
+  static const bool fuse_split = [] { const char* e = std::getenv("CASR_FUSE_SPLIT"); return !e || std::atoi(e) != 0; }();
+  bool x16_ready = false;
   for (int l = 0; l < h->cfg.enc_layers; ++l) {
     const int din = l == 0 ? D : C;
     float* out = outs[l & 1];
@@ -548,7 +552,8 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
     ProfScope ps(&h->prof, CASR_K_INPUT_PROJ, s);
     if (s16) {
       const int kp = s16_kpad(din);
-      HIP_OK(h, launch_split_rows(x, din, (int)rows, din, kp, h->x16.as<uint16_t>(), h->eflag.as<int32_t>(), s));
+      if (!x16_ready)
+        HIP_OK(h, launch_split_rows(x, din, (int)rows, din, kp, h->x16.as<uint16_t>(), h->eflag.as<int32_t>(), s));
       if (gemm16_waves() == 0)
         HIP_OK(h, launch_input_proj_s16(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
                                         h->W + h->L.enc_bias[l], h->gin.as<float>(), s));
@@ -578,7 +583,8 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
       }
       {
         ProfScope ps(&h->prof, CASR_K_REC_STEP, s);
-        HIP_OK(h, launch_rec_layer(whh, h->gin.as<float>(), xin, out,
+        uint16_t* x16o = (s16 && fuse_split && l + 1 < h->cfg.enc_layers) ? h->x16.as<uint16_t>() : nullptr;
+        HIP_OK(h, launch_rec_layer(whh, h->gin.as<float>(), xin, out, x16o,
                                    reinterpret_cast<uint32_t*>(h->hx.p), h->hfin.as<float>(),
                                    h->cst.as<float>(), dl, B, Tp, residual, s16, h->eflag.as<int32_t>(),
                                    tbuf.as<uint32_t>(), s));
@@ -596,8 +602,10 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
         }
       }
       x = out;
+      x16_ready = s16 && fuse_split;
       continue;
     }
+    x16_ready = false;
     // h (both ping-pong buffers) and c start at zero (RNN_RES state None, util.py:1236-1247)
     HIP_OK(h, fill_u32(hb, 0, (size_t)2 * 2 * B * H, s));
     HIP_OK(h, fill_u32(h->cst.p, 0, (size_t)2 * B * H, s));

@@ -196,8 +196,10 @@ int rec_layer_waves();  // waves per workgroup (trace layout)
 int rec_layer_producers();  // workgroups per row group (trace layout)
 hipError_t rec_layer_occupancy(int* blocks_per_cu);
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s);  // before EVERY launch_rec_layer
+// x16 (s16 only, may be null): also write out's s16 row image [B*Tp][C/32][32 hi | 32 lo] (the
+// next layer's input-GEMM operand, zeros past each length), replacing a split_rows pass
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
-                            uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
+                            uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s);
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s);

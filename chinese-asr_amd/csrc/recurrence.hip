@@ -80,7 +80,7 @@ CASR_DEV float decode_granule(uint32_t x) {
 template <int RG, int UW, bool S16>
 __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
-    float* __restrict__ out, uint32_t* __restrict__ hx, float* __restrict__ hfin,
+    float* __restrict__ out, uint16_t* __restrict__ x16, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
     int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg, int pre_wait, int pre_sleep) {
   constexpr int NW = RG * UW / 64;      // waves: 4 k-chunks x RG/16 row halves x UW/16 unit halves
@@ -113,6 +113,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   const int U = ub * UW + u;
   const size_t si = ((size_t)d * B + b) * H + U;       // hfin / cst index (valid when b < B)
   const size_t gi = ((size_t)d * Bp + b) * H + U;      // granule index within a buffer
+  const int x16_col = ((d * H + U) >> 5) * 64 + ((d * H + U) & 31);  // s16 image column of (d, U)
   if (tid == 0) {
     s_tmax = 0;
     s_quit[0] = s_quit[1] = 0;
@@ -267,12 +268,26 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       else  // f32 arithmetic: libm cell, torch's CPU formulas
         lstm_cell(gate[0], gate[1], gate[2], gate[3], c, h2, c2);
       c = c2;
+    }
+    // the hand-off word goes out first: the layer outputs below are off the step chain
+    if (s + 1 < tmax) store_granule<S16>(hx + (size_t)((s + 1) % 3) * 2 * plane + gi, s + 1, h2);
+    if (act) {
       const int t = (d == 0) ? s : (len - 1 - s);
       const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
       if (s == len - 1) hfin[si] = h2;
-      out[oi] = residual ? (h2 + x_res) : h2;
+      const float y = residual ? (h2 + x_res) : h2;
+      out[oi] = y;
+      // s16x3: the next layer's input row image, written here instead of by split_rows_kernel
+      if (S16 && x16) {
+        const uint32_t wv = split16_word(y);
+        uint16_t* xp = x16 + ((size_t)b * Tp + t) * (2 * C) + x16_col;
+        xp[0] = (uint16_t)wv;
+        xp[32] = (uint16_t)(wv >> 16);
+        const float m = fabsf(y);
+        if (m >= 65520.f && m < INFINITY)
+          __hip_atomic_fetch_or(err, CASR_DEV_F16_RANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
-    if (s + 1 < tmax) store_granule<S16>(hx + (size_t)((s + 1) % 3) * 2 * plane + gi, s + 1, h2);
     if (tr && lane == 0) {
       tr[s * 5 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
       tr[s * 5 + 4] = npass;
@@ -288,6 +303,13 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     }
   }
   if (b < B) cst[si] = c;
+  // padded frames of the row image are zero, as split_rows_kernel makes them from out
+  if (S16 && x16 && b < B)
+    for (int t = len; t < Tp; ++t) {
+      uint16_t* xp = x16 + ((size_t)b * Tp + t) * (2 * C) + x16_col;
+      xp[0] = 0;
+      xp[32] = 0;
+    }
 }
 
 }  // namespace
@@ -356,14 +378,14 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
 }
 
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
-                            uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
+                            uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s) {
   const int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for every layout
   const int RG = rec_rows(), UW = rec_units();
   const int nrg = (B + RG - 1) / RG;
   dim3 grid((H / UW) * nrg * 2);
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(RG * UW), 0, s, Whh_f, Gin, xin, out, hx, hfin, cst, lens, B, Bp, Tp,
+    hipLaunchKernelGGL(kern, grid, dim3(RG * UW), 0, s, Whh_f, Gin, xin, out, x16, hx, hfin, cst, lens, B, Bp, Tp,
                        residual, err, trace, nrg, rec_pre_wait(), rec_pre_sleep());
   };
   switch (rec_layout()) {
