@@ -190,18 +190,26 @@ CASR_DEV float tanh_hw(float x) {
   return copysignf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e), x);
 }
 CASR_DEV void lstm_cell_hw(float gi, float gf, float gg, float go, float c, float& h2, float& c2) {
+#pragma clang fp contract(off)  // lexical: __fmul_rn / __fadd_rn are plain * / + in their own (contracting) bodies
   const float i = sigmoid_hw(gi), f = sigmoid_hw(gf), g = tanh_hw(gg), o = sigmoid_hw(go);
-  c2 = __fadd_rn(__fmul_rn(f, c), __fmul_rn(i, g));
-  h2 = __fmul_rn(o, tanh_hw(c2));
+  c2 = f * c + i * g;  // two rounded products and a rounded add (contract off above)
+  h2 = o * tanh_hw(c2);
+}
+
+// residual add x + y of RNN_RES (util.py:1289), never fused with the cell's o * tanh(c') product
+CASR_DEV float residual_add(float y, float x) {
+#pragma clang fp contract(off)
+  return y + x;
 }
 
 // LSTM cell with PyTorch gate order (i, f, g, o): c' = f*c + i*g, h' = o*tanh(c').
 CASR_DEV void lstm_cell(float gi, float gf, float gg, float go, float c, float& h2, float& c2) {
+#pragma clang fp contract(off)  // lexical: __fmul_rn / __fadd_rn are plain * / + in their own (contracting) bodies
   const float i = sigmoid_acc(gi);
   const float f = sigmoid_acc(gf);
   const float g = tanhf(gg);
   const float o = sigmoid_acc(go);
   // no FMA contraction: torch evaluates (f * c) + (i * g) and o * tanh(c') as separate ops
-  c2 = __fadd_rn(__fmul_rn(f, c), __fmul_rn(i, g));
-  h2 = __fmul_rn(o, tanhf(c2));
+  c2 = f * c + i * g;
+  h2 = o * tanhf(c2);
 }

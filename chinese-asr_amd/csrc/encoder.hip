@@ -451,7 +451,7 @@ __global__ __launch_bounds__(256) void rec_step_kernel(
   cst[si] = c2;
   hnext[si] = h2;
   if (step == len - 1) hfin[si] = h2;
-  out[oi] = residual ? (h2 + x_res) : h2;
+  out[oi] = residual ? residual_add(h2, x_res) : h2;
 }
 
 hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,

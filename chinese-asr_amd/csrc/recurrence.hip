@@ -275,7 +275,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       const int t = (d == 0) ? s : (len - 1 - s);
       const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
       if (s == len - 1) hfin[si] = h2;
-      const float y = residual ? (h2 + x_res) : h2;
+      const float y = residual ? residual_add(h2, x_res) : h2;
       out[oi] = y;
       // s16x3: the next layer's input row image, written here instead of by split_rows_kernel
       if (S16 && x16) {
