@@ -179,8 +179,17 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       // this wave's own stores of the previous step (vmcnt(0)), then sleep pre_sleep x 64 clocks.
       // A poll issued before the group's stores have landed fails and costs a whole extra round
       // trip.  Measured (ms per greedy batch): no wait 5.95, wait + sleep 0 / 2 / 4 / 5 / 6 / 8 /
-      // 10 = 3.05 / 3.24 / 2.91 / 2.80 / 2.82-2.85 / 2.87 / 2.89; default wait + 6.
-      if (pre_wait) __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
+      // 10 = 3.05 / 3.24 / 2.91 / 2.80 / 2.82-2.85 / 2.87 / 2.89; wait + 6.  With the layer
+      // outputs stored after the hand-off word, waiting for the word alone (default 2) measured
+      // 8.29 vs 8.33 ms greedy, 9.33-9.36 vs 9.46 ms beam.
+      // pre_wait 2: wait for the hand-off word only, not for the layer-output stores issued after
+      // it (out, and with x16 the two image halves): vmcnt(3) / vmcnt(1)
+      if (pre_wait == 2) {
+        if (x16) __builtin_amdgcn_s_waitcnt(3 | (7 << 4) | (15 << 8));
+        else __builtin_amdgcn_s_waitcnt(1 | (7 << 4) | (15 << 8));
+      } else if (pre_wait) {
+        __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
+      }
       for (int i = 0; i < pre_sleep; ++i) __builtin_amdgcn_s_sleep(1);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (uint32_t pass = 0;; ++pass) {
@@ -320,7 +329,7 @@ static int env_int(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 static int rec_pre_wait() {
-  static const int v = env_int("CASR_REC_PREWAIT", 1);
+  static const int v = env_int("CASR_REC_PREWAIT", 2);  // 0 none, 1 vmcnt(0), 2 hand-off word only
   return v;
 }
 static int rec_pre_sleep() {
