@@ -528,12 +528,14 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   HIP_OK(h, h->keysT.ensure((size_t)B * A * Tq * sizeof(float)));
   HIP_OK(h, h->lens.ensure((size_t)B * sizeof(int32_t)));
   HIP_OK(h, hipMemcpyAsync(h->lens.p, lens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
-  HIP_OK(h, hipMemsetAsync(h->out0.p, 0, rows * C * sizeof(float), s));
-  HIP_OK(h, hipMemsetAsync(h->out1.p, 0, rows * C * sizeof(float), s));
+  const bool persistent = casr_recurrence_mode(h, B) == 1;
+  if (!persistent) {  // the persistent recurrence writes the padded frames itself
+    HIP_OK(h, hipMemsetAsync(h->out0.p, 0, rows * C * sizeof(float), s));
+    HIP_OK(h, hipMemsetAsync(h->out1.p, 0, rows * C * sizeof(float), s));
+  }
   HIP_OK(h, hipMemsetAsync(h->hfin.p, 0, (size_t)2 * B * H * sizeof(float), s));
   HIP_OK(h, h->eflag.ensure(16));
   HIP_OK(h, hipMemsetAsync(h->eflag.p, 0, 16, s));
-  const bool persistent = casr_recurrence_mode(h, B) == 1;
   const bool s16 = h->s16();
   if (s16) HIP_OK(h, h->x16.ensure(rows * s16_kpad(D) * sizeof(float)));
   if (persistent) HIP_OK(h, h->hx.ensure(rec_layer_granule_bytes(B)));

@@ -312,12 +312,16 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     }
   }
   if (b < B) cst[si] = c;
-  // padded frames of the row image are zero, as split_rows_kernel makes them from out
-  if (S16 && x16 && b < B)
+  // padded frames (t >= len) of the layer output and of the row image are zero (pad_packed_sequence,
+  // util.py:1307), written here so the host needs no memset of the output buffers
+  if (b < B)
     for (int t = len; t < Tp; ++t) {
-      uint16_t* xp = x16 + ((size_t)b * Tp + t) * (2 * C) + x16_col;
-      xp[0] = 0;
-      xp[32] = 0;
+      out[((size_t)b * Tp + t) * C + d * H + U] = 0.f;
+      if (S16 && x16) {
+        uint16_t* xp = x16 + ((size_t)b * Tp + t) * (2 * C) + x16_col;
+        xp[0] = 0;
+        xp[32] = 0;
+      }
     }
 }
 
