@@ -52,6 +52,7 @@ Layout make_layout(const casr_config& cfg) {
   L.emb16 = take((size_t)cfg.vocab * E);
   L.dec_w16 = take((size_t)4 * HD * KDEC);
   L.proj_w16 = take((size_t)L.VP * KPROJ);
+  L.wenc16 = take((size_t)A * C);
   L.total = off;
   return L;
 }
@@ -307,6 +308,8 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
       (!in_range(w->embedding, (size_t)cfg->vocab * E) || !in_range(w->dec_w_ih, (size_t)4 * HD * (E + C)) ||
        !in_range(w->dec_w_hh, (size_t)4 * HD * HD) || !in_range(w->proj_w, (size_t)cfg->vocab * KPROJ)))
     s16_ok = false;
+  if (w->attn_w_enc && !in_range(w->attn_w_enc, (size_t)C * A, 16.f))  // keys GEMM: the gemm16 scaling
+    s16_ok = false;
   std::memset(out, 0, L.total * sizeof(float));
   out[L.info] = s16_ok ? 1.f : 0.f;
   const int V = cfg->vocab;
@@ -368,6 +371,7 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
   for (int n = 0; n < V; ++n) out[L.proj_b + n] = w->proj_b[n];
   for (int a = 0; a < A; ++a)
     for (int c = 0; c < C; ++c) out[L.wencT + (size_t)a * C + c] = w->attn_w_enc[(size_t)c * A + a];
+  pack_rows16(out + L.wenc16, A, C, [&](int n, int k) { return out[L.wencT + (size_t)n * C + k]; });
   std::memcpy(out + L.b_attn, w->attn_b, sizeof(float) * A);
   std::memcpy(out + L.w_hidden, w->attn_w_hidden, sizeof(float) * HD * A);
   std::memcpy(out + L.v, w->attn_v, sizeof(float) * A);
@@ -585,7 +589,8 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
       }
       {
         ProfScope ps(&h->prof, CASR_K_REC_STEP, s);
-        uint16_t* x16o = (s16 && fuse_split && l + 1 < h->cfg.enc_layers) ? h->x16.as<uint16_t>() : nullptr;
+        // the last layer's image feeds the keys GEMM
+        uint16_t* x16o = (s16 && fuse_split) ? h->x16.as<uint16_t>() : nullptr;
         HIP_OK(h, launch_rec_layer(whh, h->gin.as<float>(), xin, out, x16o,
                                    reinterpret_cast<uint32_t*>(h->hx.p), h->hfin.as<float>(),
                                    h->cst.as<float>(), dl, B, Tp, residual, s16, h->eflag.as<int32_t>(),
@@ -647,7 +652,17 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   h->enc_out = const_cast<float*>(x);
   {
   ProfScope ps(&h->prof, CASR_K_KEYS, s);
-  HIP_OK(h, launch_keys(h->enc_out, B, Tp, h->W + h->L.wencT, h->W + h->L.b_attn, h->keysT.as<float>(), s));
+  // s16x3 keys on every s16 path (the per-step fallback splits the encoder output first), so both
+  // recurrences give the same keys bits
+  if (s16 && !x16_ready) {
+    HIP_OK(h, launch_split_rows(h->enc_out, C, (int)rows, C, C, h->x16.as<uint16_t>(), h->eflag.as<int32_t>(), s));
+    x16_ready = true;
+  }
+  if (x16_ready)  // s16x3 keys from the image the last persistent layer wrote
+    HIP_OK(h, launch_keys_s16(h->x16.as<float>(), B, Tp, h->W + h->L.wenc16, h->W + h->L.b_attn,
+                              h->keysT.as<float>(), s));
+  else
+    HIP_OK(h, launch_keys(h->enc_out, B, Tp, h->W + h->L.wencT, h->W + h->L.b_attn, h->keysT.as<float>(), s));
   }
   h->B = B;
   h->Tp = Tp;

@@ -51,6 +51,7 @@ struct Layout {
   size_t proj_w;                     // frag-major [VP/64 * 4][KPROJ/64], k order [ctx | h]
   size_t proj_b;                     // [VP]
   size_t wencT;                      // [A][C]
+  size_t wenc16;                     // [A][C/32][32 hi | 32 lo]: s16 row image of wencT (keys GEMM)
   size_t b_attn;                     // [A]
   size_t w_hidden;                   // [HD][A]
   size_t v;                          // [A]
@@ -201,6 +202,8 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s);  // before EVERY
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s);
+hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc16, const float* b_attn,
+                           float* keysT, hipStream_t s);
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s);
 

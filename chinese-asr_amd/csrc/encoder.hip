@@ -342,6 +342,19 @@ hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, cons
   return hipGetLastError();
 }
 
+// keys from the s16 row image of the encoder output (written by the last persistent layer) and
+// of wencT: s16x3 products, same KeysEpi store
+hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc16, const float* b_attn,
+                           float* keysT, hipStream_t s) {
+  const int M = B * Tp;
+  if (M <= 0 || C % GB_K != 0) return hipErrorInvalidValue;
+  KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3};
+  const TileOrder order = tile_order(A / GB_N, (M + GB_M - 1) / GB_M, C);
+  hipLaunchKernelGGL((gemm_nt_kernel<KeysEpi, true>), dim3(order.blocks()), dim3(256), 0, s, enc16, C, wenc16,
+                     C, M, A, C, order, epi);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ recurrence step
 // grid (H/16 unit blocks, ceil(B/16) row blocks, 2 directions), block 256.
 // S16: s16 W_hh image and s16x3 MFMAs, the h operand split in registers by the same

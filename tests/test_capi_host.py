@@ -79,6 +79,7 @@ def _layout(cfg):
     take("emb16", cfg.vocab * E)
     take("dec_w16", 4 * HD * (E + C + HD))
     take("proj_w16", VP * (C + HD))
+    take("wenc16", A * C)
     lay["total"] = off
     return lay, VP
 
@@ -150,6 +151,13 @@ def test_packed_layout_contract():
             want = blob[lay[f"wih{l}"] + n * din + k] if k < din else 0.0
             close(got, want)
             if k < din:
+                assert h16[base] == np.float16(want)
+        if l == 0:  # attention key weights: s16 row image of wencT [A][C] (keys GEMM)
+            for _ in range(20):
+                n, k = rs.randint(128), rs.randint(512)
+                base = 2 * (lay["wenc16"] + n * 512) + (k // 32) * 64 + k % 32
+                want = blob[lay["wencT"] + n * 512 + k]
+                close(float(h16[base]) + float(h16[base + 32]) / 2048.0, want)
                 assert h16[base] == np.float16(want)
         # recurrent s16 fragments: block (nt, kc) = [j][hi|lo][lane][8], k = 16(lane>>4) + 8j + e
         for _ in range(20):
