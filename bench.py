@@ -139,23 +139,19 @@ def main():
 
     from casr.config import CasrConfig
     from casr.engine import Engine
-    from casr.lib import pack_weights, load as load_lib
+    from casr.lib import pack_weights, packed_floats, load as load_lib
     from casr.weights import synthetic_state_dicts
 
     cfg = CasrConfig()
     load_lib()
     # ---- weights: pack on rank 0, RCCL broadcast of the packed blob
     t_w = time.perf_counter()
+    packed = None
     if rank == 0:
         packed = torch.from_numpy(pack_weights(cfg, *synthetic_state_dicts(cfg, peaked=True, eos_bias=0.0))).to(dev)
-        n = torch.tensor([packed.numel()], device=dev)
-    else:
-        n = torch.zeros(1, dtype=torch.int64, device=dev)
     if dist is not None:
-        dist.broadcast(n, 0)
-        if rank != 0:
-            packed = torch.empty(int(n.item()), dtype=torch.float32, device=dev)
-        dist.broadcast(packed, 0)
+        from casr.distributed import broadcast_packed
+        packed = broadcast_packed(packed, dev, expect_floats=packed_floats(cfg))
     torch.cuda.synchronize()
     weight_s = time.perf_counter() - t_w
     eng = Engine(cfg, packed=packed, device=dev)

@@ -31,15 +31,20 @@ def partition(lens, world):
     return [np.nonzero(owner == r)[0] for r in range(world)]
 
 
-def broadcast_packed(packed, device, src=0, group=None):
+def broadcast_packed(packed, device, src=0, group=None, expect_floats=None):
     """Broadcast the packed weight blob from `src`.  `packed` is a tensor on rank src (ignored
-    elsewhere).  Returns the blob on `device` on every rank."""
+    elsewhere).  Returns the blob on `device` on every rank.  With `expect_floats` (this rank's
+    casr.lib.packed_floats(cfg)) every rank checks the blob size against its own build's layout
+    before receiving it: a rank running another library version fails here, not on the device."""
     import torch.distributed as dist
     rank = dist.get_rank(group)
     n = torch.zeros(1, dtype=torch.int64, device=device)
     if rank == src:
         n[0] = packed.numel()
     dist.broadcast(n, src, group=group)
+    if expect_floats is not None and int(n.item()) != int(expect_floats):
+        raise ValueError(f"rank {rank}: broadcast blob has {int(n.item())} floats, this build's layout "
+                         f"has {int(expect_floats)}")
     if rank == src:
         buf = packed.to(device=device, dtype=torch.float32).contiguous()
     else:

@@ -12,6 +12,10 @@ import torch
 from . import lib as _lib
 from .config import CasrConfig
 
+# casr_device_flags guard bits (include/casr.h) that invalidate results
+FLAG_REC_TIMEOUT = 32   # a persistent-recurrence hand-off wait expired: that encode is invalid
+FLAG_F16_RANGE = 128    # s16x3: an activation beyond the f16 range, the split images are wrong
+
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -40,6 +44,7 @@ class Engine:
         if packed is not None:  # no weights: front-end only (log_mel / features)
             self.bind(packed)
         self._B = self._Tp = None
+        self.requested = "s16x3"
 
     def bind(self, packed):
         """packed: host numpy blob or a device tensor (e.g. received by RCCL broadcast)."""
@@ -47,6 +52,11 @@ class Engine:
             packed = torch.from_numpy(packed).to(self.device)
         if packed.device != self.device or packed.dtype != torch.float32:
             raise ValueError("packed weights must be a float32 tensor on the engine device")
+        want = _lib.packed_floats(self.cfg)
+        if packed.numel() != want:
+            # a blob packed by another build (e.g. broadcast from a rank running a different
+            # library version) would be read past its end by the kernels
+            raise ValueError(f"packed weights hold {packed.numel()} floats; this build's layout has {want}")
         self.packed = packed.contiguous()
         _lib.check(self.lib.casr_bind_weights(self.handle, _ptr(self.packed)), self.handle)
 
@@ -171,6 +181,35 @@ class Engine:
     def set_precision(self, precision):
         """'s16x3' (default: split-f16 MFMA, f32 accumulate) or 'f32' (exact-f32 MFMA)."""
         _lib.check(self.lib.casr_set_precision(self.handle, _lib.PRECISIONS[precision]), self.handle)
+        self.requested = precision
+
+    def check_flags(self):
+        """Guard bits of the last encode / decode (synchronises).  Raises CasrError when the
+        recurrence hand-off timed out (bit 32: the encode's results are invalid); returns the
+        bits otherwise, so a caller can re-run at f32 on bit 128 (FLAG_F16_RANGE)."""
+        f = self.device_flags()
+        if f & FLAG_REC_TIMEOUT:
+            raise _lib.CasrError("persistent recurrence hand-off wait expired (device flag 32): "
+                                 "the encoder results of this batch are invalid")
+        return f
+
+    def run_checked(self, encode, decode):
+        """encode(); out = decode(); then the guard bits.  Bit 32 raises; bit 128 (an s16x3
+        operand beyond the f16 range) re-runs encode + decode on the exact-f32 path, so no
+        result rests on a wrong split image."""
+        encode()
+        out = decode()
+        f = self.check_flags()
+        if f & FLAG_F16_RANGE and self.precision() == "s16x3":
+            req = self.requested
+            self.set_precision("f32")
+            try:
+                encode()
+                out = decode()
+                f = self.check_flags()
+            finally:
+                self.set_precision(req)
+        return out, f
 
     def precision(self):
         """Effective arithmetic of the MFMA contractions ('s16x3' or 'f32')."""

@@ -137,6 +137,15 @@ def config_struct(cfg):
                        cfg.sos, cfg.eos, float(cfg.temperature))
 
 
+def packed_floats(cfg):
+    """Floats in this build's packed weight layout (casr_packed_weights_floats)."""
+    c = config_struct(cfg)
+    n = int(load().casr_packed_weights_floats(ctypes.byref(c)))
+    if n == 0:
+        check(4)
+    return n
+
+
 def pack_weights(cfg, enc_sd, dec_sd):
     """Pack reference state dicts (numpy float32) into the kernel blob (host numpy array)."""
     lib = load()

@@ -17,6 +17,9 @@ namespace casr {
 
 size_t attention_smem_bytes(int k, int Tp);  // decoder.hip
 
+// version word of the packed layout (bump whenever make_layout or a packer changes)
+constexpr uint32_t LAYOUT_MAGIC = 0xCA5B0002u;
+
 Layout make_layout(const casr_config& cfg) {
   Layout L{};
   size_t off = 0;
@@ -308,10 +311,14 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
       (!in_range(w->embedding, (size_t)cfg->vocab * E) || !in_range(w->dec_w_ih, (size_t)4 * HD * (E + C)) ||
        !in_range(w->dec_w_hh, (size_t)4 * HD * HD) || !in_range(w->proj_w, (size_t)cfg->vocab * KPROJ)))
     s16_ok = false;
-  if (w->attn_w_enc && !in_range(w->attn_w_enc, (size_t)C * A, 16.f))  // keys GEMM: the gemm16 scaling
-    s16_ok = false;
+  // keys GEMM (encoder.hip gemm_nt_kernel<KeysEpi, true>): two accumulators, no 2^11 scaling of
+  // w_hi, so the f16 range limit of the other s16 images applies
+  if (w->attn_w_enc && !in_range(w->attn_w_enc, (size_t)C * A)) s16_ok = false;
   std::memset(out, 0, L.total * sizeof(float));
   out[L.info] = s16_ok ? 1.f : 0.f;
+  // layout stamp: casr_bind_weights refuses a blob packed by a build with another layout
+  const uint32_t stamp[3] = {LAYOUT_MAGIC, (uint32_t)(L.total & 0xFFFFFFFFu), (uint32_t)(L.total >> 32)};
+  std::memcpy(out + L.info + 1, stamp, sizeof stamp);
   const int V = cfg->vocab;
   for (int l = 0; l < cfg->enc_layers; ++l) {
     const int din = l == 0 ? D : C;
@@ -407,9 +414,16 @@ int casr_create(const casr_config* cfg, int device, casr_handle** out) {
 int casr_bind_weights(casr_handle* h, const float* packed_device) {
   if (!h || !packed_device) return fail(h, CASR_ERR_ARG, "handle/weights NULL");
   HIP_OK(h, hipSetDevice(h->device));
-  float info = 0.f;
-  HIP_OK(h, hipMemcpy(&info, packed_device + h->L.info, sizeof(float), hipMemcpyDeviceToHost));
-  h->s16_valid = info == 1.f;
+  float info[4] = {};
+  HIP_OK(h, hipMemcpy(info, packed_device + h->L.info, sizeof info, hipMemcpyDeviceToHost));
+  uint32_t stamp[3];
+  std::memcpy(stamp, info + 1, sizeof stamp);
+  if (stamp[0] != LAYOUT_MAGIC || stamp[1] != (uint32_t)(h->L.total & 0xFFFFFFFFu) ||
+      stamp[2] != (uint32_t)(h->L.total >> 32))
+    return fail(h, CASR_ERR_ARG,
+                "casr_bind_weights: the blob was not packed by this build's layout (stamp %08x, %u floats; "
+                "expected %08x, %zu floats)", stamp[0], stamp[1], LAYOUT_MAGIC, h->L.total);
+  h->s16_valid = info[0] == 1.f;
   h->W = packed_device;
   h->graphs.clear();  // captured graphs bake in the precision and weight pointers
   return CASR_OK;

@@ -64,6 +64,21 @@ CASR_DEV void store_granule(uint32_t* p, int step_tagged, float v) {
   __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dword sc1
 }
 
+// s_waitcnt vmcnt(min(n, 7)) (expcnt / lgkmcnt untouched): the count is an immediate, n is
+// wave-uniform
+CASR_DEV void wait_vm_upto(int n) {
+  switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8)); break;
+    case 1: __builtin_amdgcn_s_waitcnt(1 | (7 << 4) | (15 << 8)); break;
+    case 2: __builtin_amdgcn_s_waitcnt(2 | (7 << 4) | (15 << 8)); break;
+    case 3: __builtin_amdgcn_s_waitcnt(3 | (7 << 4) | (15 << 8)); break;
+    case 4: __builtin_amdgcn_s_waitcnt(4 | (7 << 4) | (15 << 8)); break;
+    case 5: __builtin_amdgcn_s_waitcnt(5 | (7 << 4) | (15 << 8)); break;
+    case 6: __builtin_amdgcn_s_waitcnt(6 | (7 << 4) | (15 << 8)); break;
+    default: __builtin_amdgcn_s_waitcnt(7 | (7 << 4) | (15 << 8)); break;
+  }
+}
+
 CASR_DEV float decode_granule(uint32_t x) {
   x &= ~TAG_BIT;
   return (x & 0x7FFFFFFFu) == NONFINITE ? __uint_as_float(0x7FC00000u) : __uint_as_float(x);
@@ -159,6 +174,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   // for the step's stores).
   // FIRST (step 0, peeled): no sweep, no MFMA.  The later steps have both unconditionally, so every
   // operand load is provably retired by the sweep's vmcnt(0) before its use.
+  int n_after = 0;  // see the end of step()
   auto step = [&](auto first_c, const int s, const float (&gin_v)[4], const float x_res, float (&gin_n)[4],
                   float& x_n) -> bool {
     constexpr bool FIRST = decltype(first_c)::value;
@@ -182,11 +198,10 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       // 10 = 3.05 / 3.24 / 2.91 / 2.80 / 2.82-2.85 / 2.87 / 2.89; wait + 6.  With the layer
       // outputs stored after the hand-off word, waiting for the word alone (default 2) measured
       // 8.29 vs 8.33 ms greedy, 9.33-9.36 vs 9.46 ms beam.
-      // pre_wait 2: wait for the hand-off word only, not for the layer-output stores issued after
-      // it (out, and with x16 the two image halves): vmcnt(3) / vmcnt(1)
+      // pre_wait 2: wait for the hand-off word only, not for the vector-memory operations this
+      // wave issued after it (n_after, counted by the previous step from what it actually issued)
       if (pre_wait == 2) {
-        if (x16) __builtin_amdgcn_s_waitcnt(3 | (7 << 4) | (15 << 8));
-        else __builtin_amdgcn_s_waitcnt(1 | (7 << 4) | (15 << 8));
+        wait_vm_upto(__builtin_amdgcn_readfirstlane(n_after));
       } else if (pre_wait) {
         __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
       }
@@ -300,6 +315,14 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     if (tr && lane == 0) {
       tr[s * 5 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
       tr[s * 5 + 4] = npass;
+    }
+    // vector-memory operations issued after the hand-off word, for the next step's pacing wait
+    // (wave-uniform; a store branch no lane of the wave takes issues nothing): the layer output,
+    // hfin on a row's last step, the two image halves, and with the trace the two stamps above plus
+    // the next step's first one.  Only the pacing depends on it: the sweep checks every tag.
+    {
+      const bool any_act = __any(act), any_last = __any(act && s == len - 1);
+      n_after = (any_act ? 1 + (any_last ? 1 : 0) + ((S16 && x16) ? 2 : 0) : 0) + (tr ? 3 : 0);
     }
     return true;
   };

@@ -89,22 +89,27 @@ class Model(object):
             self._default_int2word = load_vocab()[1]
         return self._default_int2word
 
-    def _encode(self, data, lens):
+    def _gather(self, data, lens):
         lens = torch.as_tensor(lens)
         if isinstance(data, (list, tuple)):
             feat, lens_d = self.engine.gather(list(data), lens)
         else:  # already padded [B, Tp, feat_dim]
             feat, lens_d = data.to(self.device, torch.float32), lens.to(self.device, torch.int32)
-        self.engine.encode(feat, lens_d)
-        return feat.shape[0], lens
+        return feat, lens_d, lens
+
+    def _run(self, data, lens, decode):
+        """encode + decode with the device guard bits checked (Engine.run_checked): a hand-off
+        timeout raises, an s16x3 range overflow re-runs the batch on the exact-f32 path."""
+        feat, lens_d, lens = self._gather(data, lens)
+        out, _ = self.engine.run_checked(lambda: self.engine.encode(feat, lens_d), decode)
+        return feat.shape[0], lens, out
 
     # ------------------------------------------------------------------ decode
     @torch.no_grad()
     def eval_one_batch_with_greedy(self, device, data, lens, int2word=None, text=None):
         """model.py:503-602."""
         self.model.eval()
-        bsz, lens = self._encode(data, lens)
-        out = self.engine.greedy(alignment=True)
+        bsz, lens, out = self._run(data, lens, lambda: self.engine.greedy(alignment=True))
         tokens = out['tokens'].cpu().numpy()
         out_len = out['out_len'].cpu().numpy()
         fin = out['finished'].cpu().numpy().astype(bool)
@@ -127,8 +132,7 @@ class Model(object):
                                  lm_weight=gpd['lm_weight'], length_weight=gpd['length_weight']):
         """model.py:604-987."""
         self.model.eval()
-        bsz, _ = self._encode(data, lens)
-        r = self.engine.beam(bmsz, lm_weight, length_weight)
+        bsz, _, r = self._run(data, lens, lambda: self.engine.beam(bmsz, lm_weight, length_weight))
         toks = r['tokens'].cpu().numpy()
         blen = r['length'].cpu().numpy()
         bscore = r['score'].cpu().numpy()

@@ -186,6 +186,26 @@ def test_out_of_range_weights_fall_back_to_f32_images():
     assert blob[lay["info"]] == 0.0
 
 
+def test_keys_weight_range_uses_f16_limit_and_layout_stamp():
+    """The keys GEMM's s16 images (two accumulators, no 2^11 scaling) only need the f16 range:
+    |W_enc| = 100 keeps the s16 path (the input projection's < 16 limit does not apply to it).
+    The blob carries a layout stamp (magic, total floats) after the info word, which
+    casr_bind_weights checks."""
+    enc, dec = synthetic_state_dicts(CFG)
+    dec = dict(dec)
+    w = dec["attn_mechanism.W_enc"].copy()
+    w[7, 3] = 100.0
+    dec["attn_mechanism.W_enc"] = w
+    blob = L.pack_weights(CFG, enc, dec)
+    lay, total = _layout(CFG)
+    assert blob[lay["info"]] == 1.0
+    stamp = blob[lay["info"] + 1:lay["info"] + 4].view(np.uint32)
+    assert stamp[0] == 0xCA5B0002
+    assert int(stamp[1]) | (int(stamp[2]) << 32) == blob.size == L.packed_floats(CFG)
+    w[7, 3] = 20000.0
+    assert L.pack_weights(CFG, enc, dec)[lay["info"]] == 0.0
+
+
 def test_mel_filterbank_matches_reference_fixture():
     """The library's own create_fb_matrix (data.py:21-57, float32, linspace(80, 7600, 257) bin
     quirk) against the matrix captured from the reference and against the oracle."""

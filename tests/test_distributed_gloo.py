@@ -27,7 +27,7 @@ def _worker(rank, world, port, q):
     import torch.distributed as dist
     from casr.config import CasrConfig
     from casr.distributed import broadcast_packed, gather_results, partition
-    from casr.lib import pack_weights
+    from casr.lib import pack_weights, packed_floats
     from casr.weights import synthetic_state_dicts
     from golden_util import fbank_for
     from oracle import casr_oracle as O
@@ -38,9 +38,16 @@ def _worker(rank, world, port, q):
         cfg = CasrConfig()
         enc_sd, dec_sd = synthetic_state_dicts(cfg, peaked=True)
         packed = torch.from_numpy(pack_weights(cfg, enc_sd, dec_sd)) if rank == 0 else None
-        blob = broadcast_packed(packed, torch.device("cpu"))
+        blob = broadcast_packed(packed, torch.device("cpu"), expect_floats=packed_floats(cfg))
         local_blob = pack_weights(cfg, enc_sd, dec_sd)
         same_blob = bool(np.array_equal(blob.numpy(), local_blob))
+        # a rank whose build expects another layout size refuses the blob (on every rank, before
+        # the payload broadcast, so no rank is left waiting)
+        try:
+            broadcast_packed(packed, torch.device("cpu"), expect_floats=packed_floats(cfg) + 64)
+            same_blob = False
+        except ValueError:
+            pass
         frames = [120, 45, 99, 300, 12, 60, 210]
         feats = [O.features_from_fbank(fbank_for(b, t)) for b, t in enumerate(frames)]
         lens = [f.shape[0] for f in feats]

@@ -328,3 +328,56 @@ def test_out_of_range_weights_run_f32(eng):
     # a valid blob restores the requested arithmetic
     eng.bind(pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True)))
     assert eng.precision() == eng.requested
+
+
+@pytest.mark.parametrize("name", ["plain", "peaked"])
+def test_keys_elementwise_match_oracle(eng, name):
+    """The keys GEMM alone, elementwise: keys = enc . W_enc + b_attn (attention.py:67-78) from the
+    oracle on the GPU's own encoder output, so the check isolates the keys contraction (s16x3 or
+    f32) from the encoder's.  Tolerance 2e-5 abs on |keys| <~ 3."""
+    bind(eng, name)
+    feat, flen = golden_features(eng)
+    eng.encode(feat, flen)
+    enc, _, _, keys = (x.cpu().numpy() for x in eng.encoder_results())
+    _, dec_sd = synthetic_state_dicts(CFG, peaked=(name == "peaked"))
+    for b, t in enumerate(FRAMES):
+        ref = O.compute_keys(enc[b][:, None, :], dec_sd)[:, 0, :]   # [Tp, A]
+        np.testing.assert_allclose(keys[b].T, ref, atol=2e-5, rtol=0)
+
+
+def test_bind_refuses_foreign_blob(eng):
+    """A blob of another layout (size or stamp) is refused on bind, not read past its end."""
+    from casr import lib as L
+    good = pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True))
+    with pytest.raises(ValueError):
+        eng.bind(torch.zeros(good.size + 64, dtype=torch.float32, device=eng.device))
+    at = np.nonzero(good.view(np.uint32) == 0xCA5B0002)[0]
+    assert len(at) == 1  # the layout stamp's magic word
+    bad = torch.from_numpy(good.copy()).to(eng.device)
+    bad.view(torch.int32)[int(at[0])] = 0
+    with pytest.raises(L.CasrError):
+        eng.bind(bad)
+    eng.bind(good)
+    assert eng.precision() == eng.requested
+
+
+def test_model_reruns_f32_on_f16_range_overflow():
+    """An s16x3 activation beyond the f16 range (device flag 128) would make every result after
+    it wrong: the drop-in Model re-runs such a batch on the exact-f32 path (Engine.run_checked).
+    A feature value of 1e5 forces it; the result must equal an f32-only run."""
+    import model as M
+    m = M.Model()
+    m.load_state_dicts(*synthetic_state_dicts(CFG, peaked=True))
+    dev = m.device
+    feats = [torch.from_numpy(O.features_from_fbank(fbank_for(b, t))).to(dev) for b, t in enumerate(FRAMES)]
+    feats[1] = feats[1].clone()
+    feats[1][3, 17] = 1.0e5
+    lens = torch.tensor([f.shape[0] for f in feats])
+    assert m.engine.precision() == "s16x3"
+    g = m.eval_one_batch_with_greedy(dev, feats, lens, None, None)
+    assert m.engine.precision() == "s16x3"  # restored after the f32 re-run
+    m.engine.set_precision("f32")
+    g32 = m.eval_one_batch_with_greedy(dev, feats, lens, None, None)
+    m.engine.set_precision("s16x3")
+    assert g.pred_text == g32.pred_text
+    np.testing.assert_array_equal(np.asarray(g.score), np.asarray(g32.score))
