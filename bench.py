@@ -86,6 +86,15 @@ def kernel_bytes(cls, B, Tp, R, V):
     return None
 
 
+class _StubLM:
+    """Deterministic stand-in for kenlm.LanguageModel.score (main.py:82, model.py:755): KenLM and
+    an LM file are absent offline.  Tokens arrive as private-use characters (id -> U+E000 + id)."""
+
+    def score(self, s, bos=True):
+        ids = [ord(w) - 0xE000 for w in s.split(" ") if w]
+        return -0.37 * len(ids) - 0.011 * sum(i % 97 for i in ids) - (0.5 if bos else 0.0)
+
+
 def cpu_baseline(n_utt, T):
     """The CPU oracle (numpy restatement of the reference path, oracle/casr_oracle.py) timed
     on this host on a bounded sample of the same workload."""
@@ -120,6 +129,8 @@ def main():
     ap.add_argument("--beam-steps", type=int, default=2)
     ap.add_argument("--no-beam", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the BASELINE config 2 (B=32 greedy) and config 5 (beam 16 + LM) side lines")
     ap.add_argument("--cpu-sample", type=int, default=640)
     ap.add_argument("--precision", default="s16x3", choices=["s16x3", "f32"],
                     help="MFMA arithmetic of the timed path (casr_set_precision)")
@@ -246,6 +257,62 @@ def main():
                 "rtf": dtb / args.beam_steps / (Bb * world * AUDIO_S_PER_UTT),
                 "kernel_breakdown_ms": beam_breakdown}
 
+    # BASELINE config 2: a B = 32 greedy batch (same weights, same step)
+    small = None
+    if not args.no_configs:
+        Bs = 32
+        fbs = torch.from_numpy(fbank_batch(rank * Bs, Bs, T)).to(dev)
+        frs = torch.full((Bs,), T, dtype=torch.int32, device=dev)
+
+        def step_small():
+            feat, flen = eng.features(fbs, frs)
+            eng.encode(feat, flen)
+            return eng.greedy()["tokens"].cpu()
+
+        step_small()
+        dts = timed(step_small, args.steps)
+        small = {"config": "BASELINE config 2: greedy, B=32/GPU, T=800", "batch_per_gpu": Bs,
+                 "value": Bs * world * args.steps / dts, "unit": "utt/s", "ms_per_step": 1000.0 * dts / args.steps}
+
+    # BASELINE config 5: beam 16 + second-pass LM rescoring, B = 128 per GPU (1024 on 8 GPUs).
+    # Weights with the EOS bias of the peaked recipe so hypotheses finish and the second pass has
+    # candidates to rescore; KenLM is absent offline, so the LM is a deterministic stub scored on
+    # the host (the reference also scores on the host, model.py:749-763).  Timed: features,
+    # encoder, beam decode, the finished-hypothesis records to the host and the rescoring.
+    lm_line = None
+    if not args.no_configs:
+        from casr.results import records_by_utterance, second_pass_select
+        Bl, kl = args.beam_batch, 16
+        eng5 = Engine(cfg, *synthetic_state_dicts(cfg, peaked=True), device=dev)
+        eng5.set_precision(args.precision)
+        fbl = torch.from_numpy(fbank_batch(rank * Bl, Bl, T)).to(dev)
+        frl = torch.full((Bl,), T, dtype=torch.int32, device=dev)
+        i2w = {i: chr(0xE000 + i) for i in range(cfg.vocab)}
+        lm = _StubLM()
+        info = {}
+
+        def step_lm():
+            feat, flen = eng5.features(fbl, frl)
+            eng5.encode(feat, flen)
+            r = eng5.beam(kl, 1.5, 1.5)
+            toks, blen = r["tokens"].cpu().numpy(), r["length"].cpu().numpy()
+            rt, rs, rv = (x.cpu().numpy() for x in eng5.beam_records())
+            recs = records_by_utterance(rt, rs, rv)
+            best = {b: (toks[b, :blen[b]].tolist(), 0.0) for b in range(Bl)}
+            best.update(second_pass_select(recs, i2w, lm, 1.5, 1.5))
+            info["steps"] = int(r["steps"].item())
+            info["rescored"] = sum(1 for v in recs.values() if len(v) > 1)
+            return best
+
+        step_lm()
+        dtl = timed(step_lm, args.beam_steps)
+        lm_line = {"config": "BASELINE config 5: beam 16 + second-pass LM rescoring (stub LM, host)",
+                   "k": kl, "batch_per_gpu": Bl, "value": Bl * world * args.beam_steps / dtl, "unit": "utt/s",
+                   "ms_per_step": 1000.0 * dtl / args.beam_steps, "decode_steps": info.get("steps"),
+                   "utterances_rescored": info.get("rescored"),
+                   "weights": "synthetic recipe with the EOS bias (hypotheses finish before step 40)"}
+        eng5.close()
+
     # side measurement: the same greedy step on the exact-f32 MFMA path (not the headline)
     f32_cmp = None
     if precision == "s16x3" and not args.no_f32_compare:
@@ -288,6 +355,8 @@ def main():
                              "note": "serial chain of Tp dependent steps per layer; per-step time is "
                                      "hand-off latency + MFMA + cell (DESIGN.md 3.2)"}
                             if dominant == "rec_step" else {})},
+            "config2_greedy_b32": small,
+            "config5_beam16_lm": lm_line,
             "f32_exact_path": f32_cmp,
             "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},
             "weights_bcast_s": weight_s,

@@ -95,12 +95,19 @@ def greedy_steps(out_len, finished, max_len):
 def records_by_utterance(rec_tokens, rec_score, rec_valid):
     """Finished hypotheses per utterance in the reference's list order (step, then rank):
     b -> [(tokens, score)] (model.py:715-733)."""
-    B, L, k = rec_valid.shape
+    bs, ls, cs = np.nonzero(rec_valid)  # row-major: already in (utterance, step, rank) order
+    scores = rec_score[bs, ls, cs].tolist()
+    # token lists converted per step, only the l tokens a step-l record holds
+    toks = [None] * len(bs)
+    for l in np.unique(ls).tolist():
+        sel = np.nonzero(ls == l)[0]
+        rows = rec_tokens[bs[sel], l, cs[sel], :l].tolist()
+        for i, t in zip(sel.tolist(), rows):
+            toks[i] = t
     res = {}
-    for b, l, c in zip(*np.nonzero(rec_valid)):
-        res.setdefault(int(b), []).append((int(l), int(c), rec_tokens[b, l, c, :l].tolist(),
-                                           float(rec_score[b, l, c])))
-    return {b: [(t, s) for _, _, t, s in sorted(v)] for b, v in res.items()}
+    for b, t, s in zip(bs.tolist(), toks, scores):
+        res.setdefault(b, []).append((t, s))
+    return res
 
 
 def second_pass_select(records, int2word, lm_model, lm_weight, length_weight):
@@ -112,7 +119,8 @@ def second_pass_select(records, int2word, lm_model, lm_weight, length_weight):
         if len(v) == 1:
             out[b] = v[0]
             continue
-        lm = [lm_model.score(' '.join([int2word[i] for i in t]), bos=True) for t, _ in v]
+        word = int2word.__getitem__
+        lm = [lm_model.score(' '.join(map(word, t)), bos=True) for t, _ in v]
         comb = [s + lm_weight * q + length_weight * len(t) for (t, s), q in zip(v, lm)]
         out[b] = v[int(np.argmax(comb))]
     return out

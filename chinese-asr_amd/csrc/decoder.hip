@@ -750,10 +750,16 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     const float* x = logits + (size_t)(b * k + j) * V;
     const float4* x4 = reinterpret_cast<const float4*>(x);
     const float sc = score_cur[b * k + j];
-    float lse, lt;  // the row's logsumexp; this lane's largest candidate value (for tau)
+    // the row's logsumexp; this lane's largest and second-largest candidate values (for tau)
+    float lse, lt, lt2 = -INFINITY;
+    // tau bound from the block partials only when they are at least twice as many as the 2k
+    // ranks (with as many blocks as ranks, e.g. k = 16 on 32 column blocks, the bound is the
+    // smallest block maximum: thousands of candidates pass it and the row falls back to the full
+    // selection); otherwise from the row's lane top-2s
+    const bool part_tau = UNIT_T && nbp >= 2 * n2k;
     if (UNIT_T && nbp > 0) {
       // from the projection's per-block partials (ProjEpi): lane c holds block c's max and
-      // sum exp(x - max); the 64 block maxima are distinct elements, so their 2k-th largest
+      // sum exp(x - max); the block maxima are distinct elements, so their 2k-th largest
       // bounds the row's 2k-th best value from below just as the lane maxima do
       float mb = -INFINITY, sb = 0.f;
       if (ln < nbp) {
@@ -764,39 +770,55 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
       const float s = wave_sum((sb > 0.f) ? sb * expf(mb - M) : 0.f);
       lse = logf(s) + M;
       lt = (mb - lse) + sc;
-    } else {
-      float lm = -INFINITY;  // this lane's largest x / T
+    }
+    if (!part_tau) {
+      float lm = -INFINITY, lm2 = -INFINITY;  // this lane's two largest x / T (distinct elements)
+      auto top2 = [&](float y) {
+        lm2 = fmaxf(lm2, fminf(lm, y));
+        lm = fmaxf(lm, y);
+      };
       if (vec) {
 #pragma unroll 4
         for (int i = ln; i < V / 4; i += 64) {
           const float4 q = x4[i];
-          lm = fmaxf(lm, fmaxf(fmaxf(xt(q.x), xt(q.y)), fmaxf(xt(q.z), xt(q.w))));
+          top2(xt(q.x));
+          top2(xt(q.y));
+          top2(xt(q.z));
+          top2(xt(q.w));
         }
       } else {
-        for (int v = ln; v < V; v += 64) lm = fmaxf(lm, xt(x[v]));
+        for (int v = ln; v < V; v += 64) top2(xt(x[v]));
       }
-      const float m = wave_max(lm);
-      float s = 0.f;
-      if (vec) {
+      if (!(UNIT_T && nbp > 0)) {
+        const float m = wave_max(lm);
+        float s = 0.f;
+        if (vec) {
 #pragma unroll 4
-        for (int i = ln; i < V / 4; i += 64) {
-          const float4 q = x4[i];
-          s += expf(xt(q.x) - m) + expf(xt(q.y) - m) + expf(xt(q.z) - m) + expf(xt(q.w) - m);
+          for (int i = ln; i < V / 4; i += 64) {
+            const float4 q = x4[i];
+            s += expf(xt(q.x) - m) + expf(xt(q.y) - m) + expf(xt(q.z) - m) + expf(xt(q.w) - m);
+          }
+        } else {
+          for (int v = ln; v < V; v += 64) s += expf(xt(x[v]) - m);
         }
-      } else {
-        for (int v = ln; v < V; v += 64) s += expf(xt(x[v]) - m);
+        s = wave_sum(s);
+        lse = logf(s) + m;
       }
-      s = wave_sum(s);
-      lse = logf(s) + m;
       lt = (lm - lse) + sc;
+      lt2 = (lm2 - lse) + sc;
     }
     if (j == 0) stamp(1, (uint32_t)__builtin_amdgcn_s_memrealtime());
+    // tau = the 2k-th largest of the lanes' candidate values: each round takes the largest and
+    // exposes that lane's next one
     float tau = -INFINITY;
     for (int c = 0; c < n2k; ++c) {
       const float mx = wave_max(lt);
       tau = mx;
       const unsigned long long hit = __ballot(lt == mx);
-      if (hit && ln == __ffsll((long long)hit) - 1) lt = -INFINITY;
+      if (hit && ln == __ffsll((long long)hit) - 1) {
+        lt = lt2;
+        lt2 = -INFINITY;
+      }
     }
     if (ln == 0) cnt_s[wv] = 0;
     __builtin_amdgcn_wave_barrier();

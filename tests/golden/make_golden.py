@@ -179,7 +179,7 @@ def decode_suite(name, peaked, frames, out):
     meta = {"greedy": dict(rec(g), text_len=g.text_len.tolist(), steps=len(g.alignment))}
     out[f"{name}_greedy_align_sum"] = np.stack([a.double().sum(0).numpy() for a in g.alignment])
     out[f"{name}_greedy_align_step0"] = g.alignment[0].numpy()
-    for k in (1, 4, 8):
+    for k in (1, 4, 8, 16):
         r = m.eval_one_batch_with_beam(dev, k, feats, lens, None, PUA, second_pass=False,
                                        lm_model=None, lm_weight=0.0, length_weight=0.0)
         meta[f"beam{k}"] = rec(r)
@@ -187,6 +187,10 @@ def decode_suite(name, peaked, frames, out):
     r = m.eval_one_batch_with_beam(dev, 4, feats, lens, None, PUA, second_pass=True,
                                    lm_model=StubLM(), lm_weight=1.5, length_weight=1.5)
     meta["beam4_lm"] = rec(r)
+    # BASELINE config 5: beam 16 + second pass
+    r = m.eval_one_batch_with_beam(dev, 16, feats, lens, None, PUA, second_pass=True,
+                                   lm_model=StubLM(), lm_weight=1.5, length_weight=1.5)
+    meta["beam16_lm"] = rec(r)
     r = m.eval_one_batch_with_beam(dev, 4, feats, lens, None, PUA, second_pass=False,
                                    lm_model=None, lm_weight=1.5, length_weight=1.5)
     meta["beam4_lw"] = rec(r)

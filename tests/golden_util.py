@@ -22,3 +22,13 @@ def fbank_for(b, T, n_mels=80):
 
 def golden_frames(meta):
     return [int(x) for x in meta["frames"]]
+
+
+def near_tie_beam_check(tokens, score, gold, atol, max_flips=1):
+    """Beam parity where f32 summation order can flip near-tied candidates: every score within
+    ``atol`` of the reference's, token sequences identical except for at most ``max_flips``
+    utterances (whose scores are then within ``atol`` too)."""
+    import numpy as np
+    np.testing.assert_allclose(score, gold["score"], rtol=0, atol=atol)
+    flips = [b for b, t in enumerate(tokens) if list(t) != gold["tokens"][b]]
+    assert len(flips) <= max_flips, flips

@@ -33,7 +33,7 @@ for s in $STAGES; do
       rc=$?; cat $OUT/bench.json; tail -3 $OUT/bench.err; stop_on_fault $rc bench $OUT/bench.err ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-        python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS} > $OUT/prof_bench.json 2> $OUT/prof.err
+        python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-configs ${PROF_ARGS} > $OUT/prof_bench.json 2> $OUT/prof.err
       rc=$?; tail -3 $OUT/prof.err; stop_on_fault $rc prof $OUT/prof.err
       python tools/prof_by_grid.py $OUT/prof/run_kernel_trace.csv 30 > $OUT/prof_by_grid.txt 2>&1
       head -12 $OUT/prof_by_grid.txt ;;
