@@ -157,7 +157,192 @@ __global__ __launch_bounds__(128 * WN, WN / 2) void gemm16_bias_kernel(const flo
   }
 }
 
+// ---- persistent form: one 512-thread workgroup per CU walks its tiles (the XCD-aware order
+// above, tile L = blockIdx.x + i * gridDim.x, so a workgroup stays with its XCD's weight slices)
+// and the stage pipeline runs on across tile boundaries:
+//   * the first 32-k stage of the next tile is DMA'd during the last stage of the current one,
+//     so the epilogue (slabs through the stage buffer just consumed, float4 stores to HBM)
+//     overlaps that DMA, and the stores are never waited for: the stage waits count them
+//     (vmcnt(G16P_EPI_STORES) retires the older DMA with the stores still in flight);
+//   * the DMAs are issued from inline asm (lds_dma16) and ordered by counted s_waitcnt vmcnt +
+//     raw s_barrier: no __syncthreads() (its fence drains vmcnt to 0), and hipcc inserts no wait
+//     of its own for a DMA it cannot see;
+//   * the bias of a tile arrives by one more DMA (1 KB, wave 0) into a slot beside the stages, so
+//     the epilogue reads it from LDS (a global load there would make hipcc wait vmcnt(0)).
+// Arithmetic (fragment order, MFMA order, accumulator scaling, bias add) is compute() of
+// gemm16_bias_kernel<4>: both kernels give the same bits.
+constexpr int G16P_STAGE = 2 * G16_TILE;                       // floats per stage: [A | W]
+constexpr int G16P_LDS = 2 * G16P_STAGE + 2 * G16_N;           // two stages + two bias slots
+constexpr int G16P_EPI_STORES = 32;                             // float4 stores per thread per tile
+static_assert(G16P_LDS * 4 <= 160 * 1024, "stages + bias slots fit the LDS");
+
+template <int VM>
+CASR_DEV void g16_vm_wait() {
+  static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
+}
+
+// DIAG (tools/probes/gemm16_probe.hip only; results then wrong for 1, 2, 4): 1 = no k-loop DMA
+// (stale LDS), 2 = no MFMA, 4 = no epilogue stores; 8 = iglp_opt(1) in the k loop, 16 = s_setprio 1
+// for waves 4-7 (both measured within noise)
+template <int DIAG = 0>
+__global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __restrict__ A16,
+                                                             const float* __restrict__ W16,
+                                                             const float* __restrict__ bias,
+                                                             float* __restrict__ Cout, int M, int N, int Kp,
+                                                             Order16 order, int total) {
+  __shared__ __attribute__((aligned(16))) float lds[G16P_LDS];
+  constexpr int WN = 4, NT = 2, RW = 32;  // 8 waves = 2 (M) x 4 (N) of 128 x 64; 32 staged rows per wave
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int r32 = lane & 31, hsel = lane >> 5;
+  const int G = gridDim.x, nk = Kp / G16_K;
+  float* const bias_lds = lds + 2 * G16P_STAGE;
+
+  // tiles of this workgroup: L = blockIdx.x + i G, skipping the order's empty slots
+  auto next_tile = [&](int L, int& n, int& m) {
+    while (L < total && !order.tile(L, n, m)) L += G;
+    return L;
+  };
+  // DMA of stage (tile (n, m), k tile kt) into stage buffer `sb` (+ the tile's bias at kt = 0)
+  auto stage = [&](int sb, int n, int m, int kt, int tpar) {
+    float* dst = lds + sb * G16P_STAGE;
+    const int m0 = m * G16_M, n0 = n * G16_N, k0 = kt * G16_K;
+#pragma unroll
+    for (int i = 0; i < RW / 8; ++i) {
+      const int row = wave * RW + i * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+      const int ar = min(m0 + row, M - 1), wr = min(n0 + row, N - 1);
+      float* la = dst + (wave * RW + i * 8) * G16_K;
+      lds_dma16(A16 + (size_t)ar * Kp + k0 + c * 4, la);
+      lds_dma16(W16 + (size_t)wr * Kp + k0 + c * 4, la + G16_TILE);
+    }
+    if (kt == 0 && wave == 0) lds_dma16(bias + min(n0 + lane * 4, N - 4), bias_lds + tpar * G16_N);
+  };
+
+  f32x16 acc[4][NT];
+  const _Float16 two11 = (_Float16)2048.0f;
+  if ((DIAG & 16) && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  auto compute = [&](const float* src) {
+    const float* as = src;
+    const float* ws = src + G16_TILE;
+    if constexpr ((DIAG & 8) != 0) __builtin_amdgcn_iglp_opt(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 2 * ks + hsel;
+      f16x8 wh[NT], wl[NT], w1[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int row = wn * 32 * NT + t * 32 + r32, sw = (row >> 1) & 7;
+        wh[t] = *reinterpret_cast<const f16x8*>(ws + row * G16_K + ((ch ^ sw) << 2));
+        wl[t] = *reinterpret_cast<const f16x8*>(ws + row * G16_K + (((4 + ch) ^ sw) << 2));
+        w1[t] = wh[t] * two11;
+      }
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) {
+        const int row = wm * 128 + tm * 32 + r32, sw = (row >> 1) & 7;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(as + row * G16_K + ((ch ^ sw) << 2));
+        const f16x8 al = *reinterpret_cast<const f16x8*>(as + row * G16_K + (((4 + ch) ^ sw) << 2));
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w1[t], acc[tm][t], 0, 0, 0);
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl[t], acc[tm][t], 0, 0, 0);
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh[t], acc[tm][t], 0, 0, 0);
+        }
+      }
+    }
+  };
+  auto barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  int n, m;
+  int L = next_tile(blockIdx.x, n, m);
+  if (L >= total) return;
+  int sb = 0, tpar = 0;
+  stage(0, n, m, 0, 0);
+  // the previous tile's epilogue stores issued after the DMA now waited for: all G16P_EPI_STORES
+  // of them (a full tile; the row test is wave-uniform), or fewer (then wait for everything)
+  int after_epi = 0;
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    int n2 = n, m2 = m;
+    const int L2 = next_tile(L + G, n2, m2);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (after_epi == G16P_EPI_STORES) g16_vm_wait<G16P_EPI_STORES>();
+      else g16_vm_wait<0>();
+      after_epi = 0;
+      barrier();  // everyone's DMA of this stage landed; everyone is done reading the other buffer
+      if (!(DIAG & 1)) {
+        if (kt + 1 < nk) stage(sb ^ 1, n, m, kt + 1, tpar);
+        else if (L2 < total) stage(sb ^ 1, n2, m2, 0, tpar ^ 1);
+      }
+      if (!(DIAG & 2)) compute(lds + sb * G16P_STAGE);
+      sb ^= 1;
+    }
+    // epilogue through the stage buffer just consumed (sb ^ 1 now): four rounds of two 32-row
+    // slabs (64 rows x 256 columns = the whole buffer; rows 1 KB apart and the two 32-lane halves
+    // of a ds_write_b32 are separate LDS cycles, so no padding), float4 stores + bias
+    float* slab = lds + (sb ^ 1) * G16P_STAGE;
+    const float* bl = bias_lds + tpar * G16_N;
+    const int c4 = tid & 63, r0 = tid >> 6;
+    const int m0 = m * G16_M, col = n * G16_N + c4 * 4;
+    int nst = 0;
+    barrier();  // every wave is done reading the last stage
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (wm == (p >> 1)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int tm = 2 * (p & 1) + h;
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+              slab[(h * 32 + (e & 3) + 8 * (e >> 2) + 4 * hsel) * G16_N + wn * 32 * NT + t * 32 + r32] =
+                  acc[tm][t][e] * S16_LO_INV;
+        }
+      }
+      barrier();
+      const float4 b4 = *reinterpret_cast<const float4*>(bl + c4 * 4);
+#pragma unroll
+      for (int row = r0; row < 64; row += 8) {
+        const int gr = m0 + p * 64 + row;
+        const float4 v = *reinterpret_cast<const float4*>(slab + row * G16_N + c4 * 4);
+        if ((DIAG & 4) && v.x == 12345.f) Cout[0] = b4.x;
+        if (!(DIAG & 4) && gr < M) {  // wave-uniform (row = wave + 8 j); N % 256 == 0 (host check)
+          *reinterpret_cast<float4*>(Cout + (size_t)gr * N + col) =
+              make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
+          ++nst;
+        }
+      }
+      barrier();
+    }
+    if (L2 >= total) break;
+    L = L2;
+    n = n2;
+    m = m2;
+    tpar ^= 1;
+    after_epi = nst;
+  }
+}
+
 }  // namespace
+
+// CASR_GEMM16_PERSIST: 1 (default) = gemm16_persist_kernel, 0 = gemm16_bias_kernel (A/B knob)
+static bool gemm16_persist() {
+  static const bool v = [] {
+    const char* e = std::getenv("CASR_GEMM16_PERSIST");
+    return !e || std::atoi(e) != 0;
+  }();
+  return v;
+}
 
 // CASR_GEMM16_WAVES: 8 (default) or 4 waves per 256 x 256 tile; 0 = encoder.hip's 128 x 128
 // s16 tile (tuning knob)
@@ -179,7 +364,17 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
   int NG = 1;
   while (NG < 8 && NB % (NG * 2) == 0 && (size_t)(NB / NG) * G16_N * Kp * 4 > (3u << 20)) NG *= 2;
   const Order16 order{NB, NM, NG};
-  if (gemm16_waves() == 8)
+  if (gemm16_waves() == 8 && gemm16_persist()) {
+    static int ncu = [] {
+      int dev = 0, v = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+      return v > 0 ? v : 256;
+    }();
+    const int total = order.blocks();
+    hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, M, N,
+                       Kp, order, total);
+  } else if (gemm16_waves() == 8)
     hipLaunchKernelGGL(gemm16_bias_kernel<4>, dim3(order.blocks()), dim3(512), 0, s, X16, W16, bias, Gin, M, N, Kp,
                        order);
   else
