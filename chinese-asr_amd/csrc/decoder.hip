@@ -718,8 +718,15 @@ constexpr int BS_CAP = 256;  // threshold candidates kept per row (beyond: full 
 
 // UNIT_T: temperature == 1 (the reference default, gpd['temperature']): x / T is x exactly, so the
 // three per-element divisions of each pass are skipped (bitwise the same values)
+// 8 waves, one per beam row (k = 16: two rows each).  Measured at k = 16 (B = 128): 16 waves
+// of one row each (1024 threads, <= 128 VGPRs: the register-resident row does not fit, so they
+// take the two-pass path) 45.7 us per step against 38.7 us for 8 waves on the register path.
+template <int K2>
+constexpr int bs_waves() {
+  return 8;
+}
 template <int K2, bool UNIT_T>
-__global__ __launch_bounds__(512) void beam_select_kernel(
+__global__ __launch_bounds__(64 * bs_waves<K2>()) void beam_select_kernel(
     const float* __restrict__ logits, int V, int B, int k, int l, int L, int eos, float temperature,
     const float* __restrict__ score_cur, float* __restrict__ score_next,
     int32_t* __restrict__ tok_next, int32_t* __restrict__ src_next, uint8_t* __restrict__ topfin,
@@ -728,11 +735,14 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     int32_t* __restrict__ err, GreedyPart gp, int nbp) {
   __shared__ float rv_s[KMAX_BEAM][K2];
   __shared__ int ri_s[KMAX_BEAM][K2];
+  __shared__ float rv2_s[KMAX_BEAM / 2][K2];  // block-merge tree: the other buffer of each level
+  __shared__ int ri2_s[KMAX_BEAM / 2][K2];
   __shared__ float cv[K2];
   __shared__ int ci[K2];
-  __shared__ float cv_s[8][BS_CAP];  // per-wave threshold candidates
-  __shared__ int ci_s[8][BS_CAP];
-  __shared__ int cnt_s[8];
+  constexpr int NWV = bs_waves<K2>(), NTH = 64 * NWV;
+  __shared__ float cv_s[NWV][BS_CAP];  // per-wave threshold candidates
+  __shared__ int ci_s[NWV][BS_CAP];
+  __shared__ int cnt_s[NWV];
   uint32_t* btr = g_dg_trace ? g_dg_trace + ((size_t)2 * 4096 + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int i, uint32_t v) {
     if (btr && threadIdx.x == 0) btr[i] = v;
@@ -746,12 +756,105 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
   const bool vec = (V & 3) == 0;
   auto xt = [&](float x) { return UNIT_T ? x : x / temperature; };
 
-  for (int j = wv; j < nrows; j += 8) {
+  for (int j = wv; j < nrows; j += NWV) {
     const float* x = logits + (size_t)(b * k + j) * V;
     const float4* x4 = reinterpret_cast<const float4*>(x);
     const float sc = score_cur[b * k + j];
-    // the row's logsumexp; this lane's largest and second-largest candidate values (for tau)
-    float lse, lt, lt2 = -INFINITY;
+    constexpr int QB = 20;  // float4 per lane: rows of up to 64 x 20 x 4 = 5120 logits
+    int nc;
+    float lse;  // the row's logsumexp
+    if (UNIT_T && nbp > 0 && vec && V / 4 <= 64 * QB) {
+      // one read of the row, held in registers.  Issue order: the block partials first, then the
+      // row (vector-memory loads retire in order, so the partials' wait does not drain the row
+      // loads): the row streams in under the logsumexp and tau work.
+      float mb = -INFINITY, sb = 0.f;
+      if (ln < nbp) {
+        mb = gp.mx[(size_t)(b * k + j) * GP_NB + ln];
+        sb = gp.se[(size_t)(b * k + j) * GP_NB + ln];
+      }
+      float4 q[QB];
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        const int i = ln + 64 * u;
+        q[u] = i < V / 4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const float M = wave_max(mb);
+      const float s = wave_sum((sb > 0.f) ? sb * expf(mb - M) : 0.f);
+      lse = logf(s) + M;
+      // tau bound: the block maxima when they are at least twice as many as the 2k ranks, else
+      // the lanes' top-2s of the row (with as many blocks as ranks, e.g. k = 16 on 32 column
+      // blocks, the block bound is the smallest block maximum: thousands of candidates pass it)
+      float lt, lt2 = -INFINITY;
+      if (nbp >= 2 * n2k) {
+        lt = (mb - lse) + sc;
+      } else {
+        float lm = -INFINITY, lm2 = -INFINITY;
+        auto top2 = [&](float y) {
+          lm2 = fmaxf(lm2, fminf(lm, y));
+          lm = fmaxf(lm, y);
+        };
+#pragma unroll
+        for (int u = 0; u < QB; ++u)
+          if (ln + 64 * u < V / 4) {
+            top2(q[u].x);
+            top2(q[u].y);
+            top2(q[u].z);
+            top2(q[u].w);
+          }
+        lt = (lm - lse) + sc;
+        lt2 = (lm2 - lse) + sc;
+      }
+      if (j == 0) stamp(1, (uint32_t)__builtin_amdgcn_s_memrealtime());
+      float tau = -INFINITY;  // the 2k-th largest of the lanes' candidate values
+      for (int c = 0; c < n2k; ++c) {
+        const float mx = wave_max(lt);
+        tau = mx;
+        const unsigned long long hit = __ballot(lt == mx);
+        if (hit && ln == __ffsll((long long)hit) - 1) {
+          lt = lt2;
+          lt2 = -INFINITY;
+        }
+      }
+      // candidates val >= tau, compacted per wave without atomics: per-lane counts, their
+      // exclusive prefix over the wave from bit-sliced ballots (counts < 128), then each lane
+      // writes its candidates from its offset on
+      int cnt = 0;
+#pragma unroll
+      for (int u = 0; u < QB; ++u)
+        if (ln + 64 * u < V / 4)
+          cnt += (((q[u].x - lse) + sc >= tau) ? 1 : 0) + (((q[u].y - lse) + sc >= tau) ? 1 : 0) +
+                 (((q[u].z - lse) + sc >= tau) ? 1 : 0) + (((q[u].w - lse) + sc >= tau) ? 1 : 0);
+      const unsigned long long below = (1ull << ln) - 1ull;
+      int slot = 0, total = 0;
+#pragma unroll
+      for (int bit = 0; bit < 7; ++bit) {
+        const unsigned long long mk = __ballot((cnt >> bit) & 1);
+        slot += __popcll(mk & below) << bit;
+        total += __popcll(mk) << bit;
+      }
+      auto put = [&](float val, int idx) {
+        if (val >= tau) {
+          if (slot < BS_CAP) {
+            cv_s[wv][slot] = val;
+            ci_s[wv][slot] = idx;
+          }
+          ++slot;
+        }
+      };
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        const int i = ln + 64 * u;
+        if (i < V / 4) {
+          put((q[u].x - lse) + sc, j * V + 4 * i);  // model.py:834-836
+          put((q[u].y - lse) + sc, j * V + 4 * i + 1);
+          put((q[u].z - lse) + sc, j * V + 4 * i + 2);
+          put((q[u].w - lse) + sc, j * V + 4 * i + 3);
+        }
+      }
+      nc = total;
+    } else {
+    // this lane's largest and second-largest candidate values (for tau)
+    float lt, lt2 = -INFINITY;
     // tau bound from the block partials only when they are at least twice as many as the 2k
     // ranks (with as many blocks as ranks, e.g. k = 16 on 32 column blocks, the bound is the
     // smallest block maximum: thousands of candidates pass it and the row falls back to the full
@@ -857,7 +960,10 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-    const int nc = cnt_s[wv];
+    nc = cnt_s[wv];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's candidates are in cv_s / ci_s
+    __builtin_amdgcn_wave_barrier();
     if (j == 0) {
       stamp(2, (uint32_t)__builtin_amdgcn_s_memrealtime());
       stamp(7, (uint32_t)nc);
@@ -873,14 +979,26 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
         ri_s[j][ln] = 0x7fffffff;
       }
       __builtin_amdgcn_wave_barrier();
-      for (int p = ln; p < nc; p += 64) {
-        const float pv = cv_s[wv][p];
-        const int pi = ci_s[wv][p];
+      if (nc <= 64) {  // one candidate per lane, the others read from registers (readlane)
+        const float pv = ln < nc ? cv_s[wv][ln] : -INFINITY;
+        const int pi = ln < nc ? ci_s[wv][ln] : 0x7fffffff;
         int rank = 0;
-        for (int q = 0; q < nc; ++q) rank += better(cv_s[wv][q], ci_s[wv][q], pv, pi) ? 1 : 0;
-        if (rank < n2k) {
+        for (int q = 0; q < nc; ++q)
+          rank += better(readlane_f(pv, q), __builtin_amdgcn_readlane(pi, q), pv, pi) ? 1 : 0;
+        if (ln < nc && rank < n2k) {
           rv_s[j][rank] = pv;
           ri_s[j][rank] = pi;
+        }
+      } else {
+        for (int p = ln; p < nc; p += 64) {
+          const float pv = cv_s[wv][p];
+          const int pi = ci_s[wv][p];
+          int rank = 0;
+          for (int q = 0; q < nc; ++q) rank += better(cv_s[wv][q], ci_s[wv][q], pv, pi) ? 1 : 0;
+          if (rank < n2k) {
+            rv_s[j][rank] = pv;
+            ri_s[j][rank] = pi;
+          }
         }
       }
       if (j == 0) {
@@ -906,12 +1024,57 @@ __global__ __launch_bounds__(512) void beam_select_kernel(
       if (j == 0) stamp(4, (uint32_t)__builtin_amdgcn_s_memrealtime());
     }
   }
-  __syncthreads();
-  if (wv == 0) {
-    TopList<K2> t2;
-    t2.init();
-    for (int p = ln; p < nrows * n2k; p += 64) t2.insert(rv_s[p / n2k][p % n2k], ri_s[p / n2k][p % n2k]);
-    wave_merge<K2>(t2, n2k, cv, ci);
+  __syncthreads();  // every row's sorted list is in rv_s / ri_s
+  // block merge: the rows' sorted lists are merged pairwise in a tree (nrows -> 1 in
+  // ceil(log2 nrows) levels), each level keeping the top 2k of every pair.  An entry's slot in its
+  // pair's merged list is its position in its own list + the number of entries of the other list
+  // better than it (better(): value, then lower flat index; a binary search over that sorted list),
+  // one thread per entry, every wave taking part.  Real candidates have distinct indices, so
+  // distinct slots; the (-inf, INT_MAX) sentinels that fill short lists land on slots only
+  // sentinels reach.  Same list, in the same order, as the one-wave sorted-list merge (TopList +
+  // wave_merge) this replaces.
+  {
+    float(*sv)[K2] = rv_s;
+    int(*si)[K2] = ri_s;
+    float(*dv)[K2] = rv2_s;
+    int(*di)[K2] = ri2_s;
+    int nl = nrows;
+    while (nl > 1) {
+      const int npair = nl >> 1;
+      for (int t = tid; t < npair * 2 * n2k; t += NTH) {
+        const int pr = t / (2 * n2k), side = (t / n2k) & 1, pos = t - (2 * pr + side) * n2k;
+        const float xv = sv[2 * pr + side][pos];
+        const int xi = si[2 * pr + side][pos];
+        const int o = 2 * pr + 1 - side;
+        int lo = 0, hi = n2k;  // entries of list o better than x: a prefix of it
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (better(sv[o][mid], si[o][mid], xv, xi)) lo = mid + 1;
+          else hi = mid;
+        }
+        const int slot = pos + lo;
+        if (slot < n2k) {
+          dv[pr][slot] = xv;
+          di[pr][slot] = xi;
+        }
+      }
+      if ((nl & 1) && tid < n2k) {  // an odd list out moves up unchanged
+        dv[npair][tid] = sv[nl - 1][tid];
+        di[npair][tid] = si[nl - 1][tid];
+      }
+      __syncthreads();
+      float(*tv)[K2] = sv;
+      int(*ti)[K2] = si;
+      sv = dv;
+      si = di;
+      dv = tv;
+      di = ti;
+      nl = npair + (nl & 1);
+    }
+    if (tid < n2k) {
+      cv[tid] = sv[0][tid];
+      ci[tid] = si[0][tid];
+    }
   }
   __syncthreads();
   stamp(5, (uint32_t)__builtin_amdgcn_s_memrealtime());
@@ -1202,7 +1365,7 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
 template <int K2>
 static void launch_beam_select(const DecodeArgs& a, DecodeBufs& d, int l, hipStream_t s) {
   auto kern = a.temperature == 1.0f ? beam_select_kernel<K2, true> : beam_select_kernel<K2, false>;
-  hipLaunchKernelGGL(kern, dim3(a.B), dim3(512), 0, s, d.logits, a.V, a.B, a.k, l,
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(64 * bs_waves<K2>()), 0, s, d.logits, a.V, a.B, a.k, l,
                      a.max_len, a.eos, a.temperature, d.score[l & 1], d.score[(l + 1) & 1],
                      d.tok[(l + 1) & 1], d.src[(l + 1) & 1], d.topfin, d.bp, d.tk, d.rec_score,
                      d.rec_src, d.rec_valid, d.newdone, d.err, d.part, row_partials(a) ? proj_col_blocks(a) : 0);

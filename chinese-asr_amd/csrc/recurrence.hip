@@ -270,12 +270,19 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) rb[w][tn][lane] = acc[tn];
     __syncthreads();
-    if (s_quit[s & 1]) return false;
+    // the 16 k-chunk partials of this cell and the quit flag in one round of LDS reads (the quit
+    // test used to go first: one more LDS round trip on the step chain)
+    const int hw = ((rl >> 4) + (RG / 16) * (u >> 4)) * 4, rr = rl & 15;
+    const int src_lane = (u & 15) + 16 * (rr >> 2), reg = rr & 3;
+    float part[4][4];
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) part[tn][ww] = rb[hw + ww][tn][src_lane][reg];
+    const int quit = s_quit[s & 1];  // acted on below, before the first store of the step
     if (tr && lane == 0) tr[s * 5 + 2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 
     // cell (same reduction order as rec_step_kernel: k-chunks 0..3, then + Gin)
-    const int hw = ((rl >> 4) + (RG / 16) * (u >> 4)) * 4, rr = rl & 15;
-    const int src_lane = (u & 15) + 16 * (rr >> 2), reg = rr & 3;
     float h2 = 0.f;
     if (act) {
       float gate[4];
@@ -283,7 +290,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       for (int tn = 0; tn < 4; ++tn) {
         float sum = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) sum += rb[hw + ww][tn][src_lane][reg];
+        for (int ww = 0; ww < 4; ++ww) sum += part[tn][ww];
         gate[tn] = sum + gin_v[tn];
       }
       float c2;
@@ -293,6 +300,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
         lstm_cell(gate[0], gate[1], gate[2], gate[3], c, h2, c2);
       c = c2;
     }
+    if (quit) return false;
     // the hand-off word goes out first: the layer outputs below are off the step chain
     if (s + 1 < tmax) store_granule<S16>(hx + (size_t)((s + 1) % 3) * 2 * plane + gi, s + 1, h2);
     if (act) {

@@ -29,6 +29,20 @@ def attn_report(r, title):
         print(f"  {n:14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
     v = t[:, 0]
     print(f"  {'start':14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
+def gemm_report(raw, tag):
+    for cls, name in ((0, "dec_lstm"), (1, "proj")):
+        r = raw[cls]
+        r = r[r[:, 0] > 0]
+        t = (r[:, :5] - r[:, 0].min()) * 10 / 1000.0  # us
+        span = t[:, 4].max()
+        ph = {"start": t[:, 0], "prologue": t[:, 1] - t[:, 0], "first tile": t[:, 2] - t[:, 1],
+              "k loop": t[:, 3] - t[:, 2], "epilogue": t[:, 4] - t[:, 3], "block": t[:, 4] - t[:, 0]}
+        print(f"{name} ({tag}): {len(r)} blocks, span {span:.2f} us")
+        for k, v in ph.items():
+            print(f"  {k:12s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  "
+                  f"p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f}")
+
+
 cfg = CasrConfig()
 eng = Engine(cfg, *synthetic_state_dicts(cfg, peaked=True, eos_bias=0.0))
 fb = torch.from_numpy(np.stack([np.random.RandomState(1234 + b).standard_normal((T, 80)).astype(np.float32)
@@ -39,13 +53,15 @@ eng.greedy()["tokens"].cpu()
 eng.greedy()["tokens"].cpu()
 if os.environ.get("BEAM"):
     eng.encode(feat[:128].contiguous(), flen[:128].contiguous())
-    eng.beam(8)["tokens"].cpu()
-    eng.beam(8)["tokens"].cpu()
+    kb = int(os.environ.get("K", 8))
+    eng.beam(kb)["tokens"].cpu()
+    eng.beam(kb)["tokens"].cpu()
     raw = np.fromfile(PATH, dtype=np.uint32).reshape(4, 4096, 8).astype(np.int64)
     r = raw[2]
     r = r[r[:, 0] > 0]
     t = (r[:, :7] - r[:, 0].min()) * 10 / 1000.0
     attn_report(raw[3], "attention (beam)")
+    gemm_report(raw, "beam")
     names = ["lse+partials", "tau+offer", "list insert", "row merge", "block merge", "bookkeeping"]
     print(f"beam_select: {len(r)} blocks, span {t[:, 6].max():.2f} us, candidates (wave 0) p50 {np.median(r[:, 7]):.0f} max {r[:, 7].max()}")
     for i, n in enumerate(names):
@@ -54,13 +70,4 @@ if os.environ.get("BEAM"):
     sys.exit(0)
 raw = np.fromfile(PATH, dtype=np.uint32).reshape(4, 4096, 8).astype(np.int64)
 attn_report(raw[3], "attention (greedy)")
-for cls, name in ((0, "dec_lstm"), (1, "proj")):
-    r = raw[cls]
-    r = r[r[:, 0] > 0]
-    t = (r[:, :5] - r[:, 0].min()) * 10 / 1000.0  # us
-    span = t[:, 4].max()
-    ph = {"start": t[:, 0], "prologue": t[:, 1] - t[:, 0], "first tile": t[:, 2] - t[:, 1],
-          "k loop": t[:, 3] - t[:, 2], "epilogue": t[:, 4] - t[:, 3], "block": t[:, 4] - t[:, 0]}
-    print(f"{name}: {len(r)} blocks, span {span:.2f} us")
-    for k, v in ph.items():
-        print(f"  {k:12s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f}")
+gemm_report(raw, "greedy")
