@@ -728,7 +728,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   if (smem > 160 * 1024)
     return fail(h, CASR_ERR_UNSUPPORTED, "attention needs %zu B of LDS (k=%d, Tp=%d) > 160 KiB", smem, k, Tp);
   HIP_OK(h, h->st.ensure(((size_t)2 * R * ST + (size_t)(HD / 16) * R * A) * sizeof(float)));
-  HIP_OK(h, h->logits.ensure(((size_t)R * V + (size_t)3 * R * GP_NB) * sizeof(float)));
+  HIP_OK(h, h->logits.ensure(((size_t)R * V + (size_t)3 * R * GP_NB + (size_t)R * GP_NT) * sizeof(float)));
   HIP_OK(h, h->small.ensure((size_t)(6 * R + L + B + R + 1) * sizeof(int32_t) + 256));
   HIP_OK(h, h->bp.ensure((size_t)L * R * sizeof(int32_t)));
   HIP_OK(h, h->tk.ensure((size_t)L * R * sizeof(int32_t)));
@@ -741,6 +741,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   d.part.mx = d.logits + (size_t)R * V;
   d.part.se = d.part.mx + (size_t)R * GP_NB;
   d.part.ix = reinterpret_cast<int32_t*>(d.part.se + (size_t)R * GP_NB);
+  d.part.tmx = reinterpret_cast<float*>(d.part.ix + (size_t)R * GP_NB);
   int32_t* sp = h->small.as<int32_t>();
   d.tok[0] = sp;
   d.tok[1] = sp + R;

@@ -214,7 +214,9 @@ struct GreedyPart {
   float* mx;    // [R][GP_NB] block maximum of the row's logits
   float* se;    // [R][GP_NB] sum exp(x - block maximum)
   int32_t* ix;  // [R][GP_NB] first column of the block maximum
+  float* tmx;   // [R][GP_NT] maximum of each 16-column tile (beam at temperature 1), or nullptr
 };
+constexpr int GP_NT = 320;  // 16-column tiles per row (V <= 5120)
 
 struct DecodeBufs {
   float* st[2];          // [R][ST]

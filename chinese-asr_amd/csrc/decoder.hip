@@ -267,7 +267,11 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       for (int tn = 0; tn < NT; ++tn) acc[tn] += part[((j * WR + ws) * NT + tn) * 64 + lane];
   }
   // lane holds rows rb*BM + ws*16 + 4g + e (e = 0..3), column (nb*NT + tn)*16 + r
-  epi.template run<NT>(acc, erow0, nb, r, pre);
+  // per-wave LDS scratch for the epilogue (ring buffers are free now; the k-slice exchange
+  // above used lb0, and waves with ws < 4 take lb1): 16 rows x (16 NT + 4) floats
+  static_assert(4 * 16 * (16 * NT + 4) <= STG, "epilogue slabs fit a stage buffer");
+  float* escr = (ws < 4 ? lb1 : lb0) + (ws & 3) * 16 * (16 * NT + 4);
+  epi.template run<NT>(acc, erow0, nb, r, pre, escr);
   stamp(4);
 }
 
@@ -351,7 +355,7 @@ struct DecLstmEpi {
     for (int e = 0; e < 4; ++e) p.cold[e] = st_old[(size_t)p.srow[e] * ST + C + HD + U];
   }
   template <int NTN = 4>
-  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p) const {
+  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p, float*) const {
     static_assert(NTN == 4, "the LSTM cell needs the 4 gate tiles of a 64-column block");
     __shared__ float ht[8][16][17];  // per row-slab wave (<= 8 per block): h tile [row][unit]
     const int lane = threadIdx.x & 63, ws = (row0 >> 4) & 7, g = lane >> 4;
@@ -427,16 +431,48 @@ struct ProjEpi {
   }
   __device__ __forceinline__ void late(Pre&, int, int, int) const {}
   template <int NTN = 4>
-  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p) const {
+  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p,
+                                      float* scr) const {
     static_assert(NTN <= 16, "bias prefetch slots");
     if (logits) {
+      // beam: the wave's 16 rows x 16 NTN columns go through its LDS slab (row stride padded by 4
+      // floats: the four row groups of a column write hit different banks), then out as float4
+      // row segments (one instruction covers 64 consecutive float4 of the tile, row-major: up to
+      // 640 contiguous bytes per row), and each 16-column tile's maximum (gp.tmx, for the
+      // select's threshold and candidate tiles) is reduced over the quad of lanes that hold it
+      constexpr int RWS = 16 * NTN + 4, CH = 4 * NTN;  // slab row stride; float4 per tile row
+      const int lane = threadIdx.x & 63, g = lane >> 4;
 #pragma unroll
-      for (int tn = 0; tn < NTN; ++tn) {
-        const int n = (nb * NTN + tn) * 16 + u;
-        if (n >= V) continue;
+      for (int tn = 0; tn < NTN; ++tn)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (row0 + e < R) logits[(size_t)(row0 + e) * V + n] = acc[tn][e] + p.bn[tn];
+        for (int e = 0; e < 4; ++e) scr[(4 * g + e) * RWS + tn * 16 + u] = acc[tn][e] + p.bn[tn];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const int rb0 = row0 - 4 * g, c0 = nb * 16 * NTN;
+      const bool vec = (V & 3) == 0;
+#pragma unroll
+      for (int i = 0; i < CH / 4; ++i) {
+        const int f = i * 64 + lane, rr = f / CH, ch = f - rr * CH;
+        const float4 v = *reinterpret_cast<const float4*>(scr + rr * RWS + 4 * ch);
+        const int row = rb0 + rr, col = c0 + 4 * ch;
+        if (row < R) {
+          float* dst = logits + (size_t)row * V + col;
+          if (vec && col + 3 < V) {
+            *reinterpret_cast<float4*>(dst) = v;
+          } else {
+            if (col < V) dst[0] = v.x;
+            if (col + 1 < V) dst[1] = v.y;
+            if (col + 2 < V) dst[2] = v.z;
+            if (col + 3 < V) dst[3] = v.w;
+          }
+        }
+        if (gp.tmx) {
+          float m = fmaxf(fmaxf(col < V ? v.x : -INFINITY, col + 1 < V ? v.y : -INFINITY),
+                          fmaxf(col + 2 < V ? v.z : -INFINITY, col + 3 < V ? v.w : -INFINITY));
+          m = fmaxf(m, dpp_f<DPP_XOR1>(m));
+          m = fmaxf(m, dpp_f<DPP_XOR2>(m));
+          if ((lane & 3) == 0 && row < R) gp.tmx[(size_t)row * GP_NT + (col >> 4)] = m;
+        }
       }
     }
     if (!gp.mx) return;
@@ -760,70 +796,103 @@ __global__ __launch_bounds__(64 * bs_waves<K2>()) void beam_select_kernel(
     const float* x = logits + (size_t)(b * k + j) * V;
     const float4* x4 = reinterpret_cast<const float4*>(x);
     const float sc = score_cur[b * k + j];
-    constexpr int QB = 20;  // float4 per lane: rows of up to 64 x 20 x 4 = 5120 logits
+    constexpr int TPL = GP_NT / 64;  // tile maxima per lane
     int nc;
     float lse;  // the row's logsumexp
-    if (UNIT_T && nbp > 0 && vec && V / 4 <= 64 * QB) {
-      // one read of the row, held in registers.  Issue order: the block partials first, then the
-      // row (vector-memory loads retire in order, so the partials' wait does not drain the row
-      // loads): the row streams in under the logsumexp and tau work.
+    if (UNIT_T && nbp > 0 && gp.tmx && vec) {
+      // From the projection's partials: block (max, sum exp) -> logsumexp, and the maximum of
+      // every 16-column tile.  tau = the exact 2k-th largest tile maximum (in candidate value,
+      // monotone in x): the tile maxima are distinct elements, so tau bounds the row's 2k-th best
+      // value from below, and every element of the top 2k lies in a tile whose maximum is >= tau.
+      // Only those tiles (2k of them, ties aside) are read: 16 logits each instead of the row.
+      const size_t row = (size_t)(b * k + j);
       float mb = -INFINITY, sb = 0.f;
       if (ln < nbp) {
-        mb = gp.mx[(size_t)(b * k + j) * GP_NB + ln];
-        sb = gp.se[(size_t)(b * k + j) * GP_NB + ln];
+        mb = gp.mx[row * GP_NB + ln];
+        sb = gp.se[row * GP_NB + ln];
       }
-      float4 q[QB];
+      const int ntile = (V + 15) / 16;
+      float tm[TPL];
+      int tt[TPL];
 #pragma unroll
-      for (int u = 0; u < QB; ++u) {
-        const int i = ln + 64 * u;
-        q[u] = i < V / 4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int c = 0; c < TPL; ++c) {
+        tt[c] = ln + 64 * c;
+        tm[c] = tt[c] < ntile ? gp.tmx[row * GP_NT + tt[c]] : -INFINITY;
       }
       const float M = wave_max(mb);
       const float s = wave_sum((sb > 0.f) ? sb * expf(mb - M) : 0.f);
       lse = logf(s) + M;
-      // tau bound: the block maxima when they are at least twice as many as the 2k ranks, else
-      // the lanes' top-2s of the row (with as many blocks as ranks, e.g. k = 16 on 32 column
-      // blocks, the block bound is the smallest block maximum: thousands of candidates pass it)
-      float lt, lt2 = -INFINITY;
-      if (nbp >= 2 * n2k) {
-        lt = (mb - lse) + sc;
-      } else {
-        float lm = -INFINITY, lm2 = -INFINITY;
-        auto top2 = [&](float y) {
-          lm2 = fmaxf(lm2, fminf(lm, y));
-          lm = fmaxf(lm, y);
-        };
+      // this lane's tiles in descending maximum (a 5-element sorting network of swaps)
 #pragma unroll
-        for (int u = 0; u < QB; ++u)
-          if (ln + 64 * u < V / 4) {
-            top2(q[u].x);
-            top2(q[u].y);
-            top2(q[u].z);
-            top2(q[u].w);
+      for (int i = 0; i < TPL; ++i)
+#pragma unroll
+        for (int c = 0; c + 1 < TPL - i; ++c)
+          if (tm[c + 1] > tm[c]) {
+            const float fv = tm[c];
+            tm[c] = tm[c + 1];
+            tm[c + 1] = fv;
+            const int iv = tt[c];
+            tt[c] = tt[c + 1];
+            tt[c + 1] = iv;
           }
-        lt = (lm - lse) + sc;
-        lt2 = (lm2 - lse) + sc;
-      }
+      // each lane's best tile is read ahead, under the tau rounds (the qualifying tiles are the
+      // 2k best, most of them each the best of its lane); the rest only if they qualify.  Reading
+      // the two best ahead measured the same.
+      constexpr int PRE = 1;
+      float4 xq[TPL][4];
+#pragma unroll
+      for (int c = 0; c < PRE; ++c)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) xq[c][h] = x4[min(tt[c], ntile - 1) * 4 + h];
       if (j == 0) stamp(1, (uint32_t)__builtin_amdgcn_s_memrealtime());
-      float tau = -INFINITY;  // the 2k-th largest of the lanes' candidate values
-      for (int c = 0; c < n2k; ++c) {
-        const float mx = wave_max(lt);
-        tau = mx;
-        const unsigned long long hit = __ballot(lt == mx);
-        if (hit && ln == __ffsll((long long)hit) - 1) {
-          lt = lt2;
-          lt2 = -INFINITY;
+      float tau = -INFINITY;
+      {
+        float hd[TPL];  // this lane's remaining tile maxima, head first
+#pragma unroll
+        for (int c = 0; c < TPL; ++c) hd[c] = (tm[c] - lse) + sc;
+        for (int c = 0; c < n2k; ++c) {
+          const float mx = wave_max(hd[0]);
+          tau = mx;
+          const unsigned long long hit = __ballot(hd[0] == mx);
+          if (hit && ln == __ffsll((long long)hit) - 1) {
+#pragma unroll
+            for (int i = 0; i + 1 < TPL; ++i) hd[i] = hd[i + 1];
+            hd[TPL - 1] = -INFINITY;
+          }
         }
       }
-      // candidates val >= tau, compacted per wave without atomics: per-lane counts, their
-      // exclusive prefix over the wave from bit-sliced ballots (counts < 128), then each lane
-      // writes its candidates from its offset on
+      // the qualifying tiles' logits (all loads issued before any use), then the candidates
+      // val >= tau compacted per wave without atomics: per-lane counts, their exclusive prefix over
+      // the wave from bit-sliced ballots (counts <= 80 < 128), each lane writing from its offset
+      bool qual[TPL];
+#pragma unroll
+      for (int c = 0; c < TPL; ++c) {
+        qual[c] = (tm[c] - lse) + sc >= tau;
+        if (c >= PRE) {
+#pragma unroll
+          for (int h = 0; h < 4; ++h)
+            xq[c][h] = qual[c] ? x4[tt[c] * 4 + h] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+        }
+      }
+      // per-slot 16-bit hit masks; a slot no lane of the wave qualifies in (the usual case past the
+      // lanes' best tiles) is skipped by a wave-uniform branch
+      uint32_t hm[TPL];
       int cnt = 0;
 #pragma unroll
-      for (int u = 0; u < QB; ++u)
-        if (ln + 64 * u < V / 4)
-          cnt += (((q[u].x - lse) + sc >= tau) ? 1 : 0) + (((q[u].y - lse) + sc >= tau) ? 1 : 0) +
-                 (((q[u].z - lse) + sc >= tau) ? 1 : 0) + (((q[u].w - lse) + sc >= tau) ? 1 : 0);
+      for (int c = 0; c < TPL; ++c) {
+        hm[c] = 0u;
+        if (__ballot(qual[c])) {
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const int n0 = tt[c] * 16 + 4 * h;
+            const float xs[4] = {xq[c][h].x, xq[c][h].y, xq[c][h].z, xq[c][h].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              hm[c] |= (qual[c] && n0 + e < V && (xs[e] - lse) + sc >= tau) ? (1u << (4 * h + e)) : 0u;
+          }
+          cnt += __popc(hm[c]);
+        }
+      }
       const unsigned long long below = (1ull << ln) - 1ull;
       int slot = 0, total = 0;
 #pragma unroll
@@ -832,23 +901,23 @@ __global__ __launch_bounds__(64 * bs_waves<K2>()) void beam_select_kernel(
         slot += __popcll(mk & below) << bit;
         total += __popcll(mk) << bit;
       }
-      auto put = [&](float val, int idx) {
-        if (val >= tau) {
-          if (slot < BS_CAP) {
-            cv_s[wv][slot] = val;
-            ci_s[wv][slot] = idx;
-          }
-          ++slot;
-        }
-      };
 #pragma unroll
-      for (int u = 0; u < QB; ++u) {
-        const int i = ln + 64 * u;
-        if (i < V / 4) {
-          put((q[u].x - lse) + sc, j * V + 4 * i);  // model.py:834-836
-          put((q[u].y - lse) + sc, j * V + 4 * i + 1);
-          put((q[u].z - lse) + sc, j * V + 4 * i + 2);
-          put((q[u].w - lse) + sc, j * V + 4 * i + 3);
+      for (int c = 0; c < TPL; ++c) {
+        if (__ballot(hm[c] != 0u)) {
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const int n0 = tt[c] * 16 + 4 * h;
+            const float xs[4] = {xq[c][h].x, xq[c][h].y, xq[c][h].z, xq[c][h].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if ((hm[c] >> (4 * h + e)) & 1u) {
+                if (slot < BS_CAP) {
+                  cv_s[wv][slot] = (xs[e] - lse) + sc;  // model.py:834-836
+                  ci_s[wv][slot] = j * V + n0 + e;
+                }
+                ++slot;
+              }
+          }
         }
       }
       nc = total;
@@ -1293,7 +1362,8 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
     ProjA asrc{st_new, R, a.s16};
     // greedy: per-block partials instead of logits; beam at temperature 1: logits and partials
     const bool parts = row_partials(a);
-    const GreedyPart gp = parts ? d.part : GreedyPart{nullptr, nullptr, nullptr};
+    GreedyPart gp = parts ? d.part : GreedyPart{nullptr, nullptr, nullptr, nullptr};
+    if (a.greedy_run || a.V > 16 * GP_NT) gp.tmx = nullptr;  // tile maxima: beam only
     ProjEpi epi{a.W + a.L.proj_b, a.greedy_run && parts ? nullptr : d.logits, d.newdone, R, a.V, l, total, d.err, gp};
     launch_proj(R, a.L.VP / 16, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, s);
   }
