@@ -120,6 +120,19 @@ class Engine:
         self._B, self._Tp = B, Tp
         self._lens = lens
 
+    def encode_fbank(self, fbank, frames, eps=1e-6):
+        """features + encode in one call (casr_encode_fbank): fbank [B, T, n_mels] float32 and
+        frames [B] int32 on the device; the features stay inside the handle (s16x3: written
+        straight as the layer-0 split-f16 image).  Returns feat_len [B] int32 (= frames // 3)."""
+        fbank = fbank.contiguous()
+        B, T, _ = fbank.shape
+        flen = torch.empty(B, device=self.device, dtype=torch.int32)
+        _lib.check(self.lib.casr_encode_fbank(self.handle, _ptr(fbank), _ptr(frames.to(torch.int32).contiguous()),
+                                              B, T, ctypes.c_float(eps), _ptr(flen), _stream()), self.handle)
+        self._B, self._Tp = B, T // 3
+        self._lens = flen
+        return flen
+
     def encoder_results(self):
         B, Tp, Cz = self._B, self._Tp, 2 * self.cfg.enc_hidden
         enc = torch.empty(B, Tp, Cz, device=self.device)

@@ -18,7 +18,7 @@ STATUS = {0: "CASR_OK", 1: "CASR_ERR_ARG", 2: "CASR_ERR_HIP", 3: "CASR_ERR_STATE
 EXPORTS = [
     "casr_api_version", "casr_packed_weights_floats", "casr_pack_weights", "casr_create",
     "casr_bind_weights", "casr_destroy", "casr_last_error", "casr_features",
-    "casr_gather_utterances", "casr_encode", "casr_encoder_results", "casr_greedy", "casr_beam",
+    "casr_gather_utterances", "casr_encode", "casr_encode_fbank", "casr_encoder_results", "casr_greedy", "casr_beam",
     "casr_beam_records", "casr_profile_enable", "casr_profile_read", "casr_set_graphs",
     "casr_device_flags", "casr_set_persistent", "casr_recurrence_mode", "casr_log_mel",
     "casr_log_mel_frames", "casr_mel_filterbank", "casr_set_precision", "casr_get_precision",
@@ -84,6 +84,7 @@ def load(path=None):
         "casr_features": (i32, [vp, vp, vp, i32, i32, f32, vp, vp, vp]),
         "casr_gather_utterances": (i32, [vp, vp, vp, i32, i32, vp, vp]),
         "casr_encode": (i32, [vp, vp, vp, i32, i32, vp]),
+        "casr_encode_fbank": (i32, [vp, vp, vp, i32, i32, f32, vp, vp]),
         "casr_encoder_results": (i32, [vp, vp, vp, vp, vp, vp]),
         "casr_greedy": (i32, [vp, vp, vp, vp, vp, vp, vp]),
         "casr_beam": (i32, [vp, i32, f32, f32, vp, vp, vp, vp, vp]),
@@ -104,7 +105,7 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.casr_api_version() != 1:
+    if lib.casr_api_version() != 2:
         raise CasrError("casr library API version mismatch")
     _LIB = lib
     return lib

@@ -162,6 +162,7 @@ struct casr_handle {
   std::string err;
   // encoder workspace
   DevBuf gin, out0, out1, hbuf, cst, hfin, keysT, lens;
+  DevBuf feat;     // casr_encode_fbank outside the s16x3 image path: the f32 features
   DevBuf hx;       // persistent recurrence: tagged h words [3][2][Bp][H]
   DevBuf eflag;    // encoder device guard bits (CASR_DEV_REC_TIMEOUT)
   DevBuf fe_const; // FrontendConst (filterbank, window, twiddles), built on first casr_log_mel
@@ -452,7 +453,7 @@ void casr_destroy(casr_handle* h) {
     if (h->ev_out[i]) (void)hipEventDestroy(h->ev_out[i]);
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
-  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->hx, &h->x16, &h->eflag, &h->fe_const, &h->fflag,
+  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->hx, &h->x16, &h->eflag, &h->fe_const, &h->fflag,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout})
     b->release();
   delete h;
@@ -529,12 +530,11 @@ int casr_gather_utterances(casr_handle* h, const float* const* utt_ptrs, const i
   return CASR_OK;
 }
 
-int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, int Tp, void* stream) {
-  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
-  if (!h->W) return fail(h, CASR_ERR_STATE, "casr_encode: no weights bound");
-  if (!feat || !lens || B <= 0 || Tp <= 0) return fail(h, CASR_ERR_ARG, "casr_encode: bad arguments");
-  HIP_OK(h, hipSetDevice(h->device));
-  hipStream_t s = (hipStream_t)stream;
+// The encoder.  fb != nullptr (casr_encode_fbank): the inputs are fbank [B][T][n_mels] + frames
+// and the features are computed here (s16x3: straight into the layer-0 row image); otherwise
+// feat [B][Tp][feat_dim] + lens.
+static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, int B, int Tp, hipStream_t s,
+                       const float* fb = nullptr, const int32_t* frames = nullptr, int T = 0, float eps = 0.f) {
   const size_t rows = (size_t)B * Tp;
   HIP_OK(h, h->gin.ensure(rows * 8 * H * sizeof(float)));
   HIP_OK(h, h->out0.ensure(rows * C * sizeof(float)));
@@ -545,7 +545,7 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   const int Tq = (Tp + 3) & ~3;  // keysT row stride (16 B aligned rows for the attention)
   HIP_OK(h, h->keysT.ensure((size_t)B * A * Tq * sizeof(float)));
   HIP_OK(h, h->lens.ensure((size_t)B * sizeof(int32_t)));
-  HIP_OK(h, hipMemcpyAsync(h->lens.p, lens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  if (!fb) HIP_OK(h, hipMemcpyAsync(h->lens.p, lens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
   const bool persistent = casr_recurrence_mode(h, B) == 1;
   if (!persistent) {  // the persistent recurrence writes the padded frames itself
     HIP_OK(h, hipMemsetAsync(h->out0.p, 0, rows * C * sizeof(float), s));
@@ -559,12 +559,24 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   if (persistent) HIP_OK(h, h->hx.ensure(rec_layer_granule_bytes(B)));
   const int32_t* dl = h->lens.as<int32_t>();
   float* outs[2] = {h->out0.as<float>(), h->out1.as<float>()};
+  bool x16_ready = false;
+  if (fb) {
+    ProfScope ps(&h->prof, CASR_K_FEATURES, s);
+    if (s16 && features_x16_supported(T)) {
+      HIP_OK(h, launch_features_x16(fb, frames, B, T, eps, h->lens.as<int32_t>(), h->x16.as<uint16_t>(), s16_kpad(D),
+                                    h->eflag.as<int32_t>(), s));
+      x16_ready = true;  // feat stays NULL: layer 0 reads only the image (no residual input)
+    } else {
+      HIP_OK(h, h->feat.ensure(rows * D * sizeof(float)));
+      HIP_OK(h, launch_features(fb, frames, B, T, eps, h->feat.as<float>(), h->lens.as<int32_t>(), s));
+      feat = h->feat.as<float>();
+    }
+  }
   const float* x = feat;
   float* hb = h->hbuf.as<float>();
   // s16: a persistent layer writes the next layer's input row image itself (no split pass);
   // CASR_FUSE_SPLIT=0 restores the separate split_rows pass (A/B knob)
   static const bool fuse_split = [] { const char* e = std::getenv("CASR_FUSE_SPLIT"); return !e || std::atoi(e) != 0; }();
-  bool x16_ready = false;
   for (int l = 0; l < h->cfg.enc_layers; ++l) {
     const int din = l == 0 ? D : C;
     float* out = outs[l & 1];
@@ -683,6 +695,28 @@ int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, i
   h->encoded = true;
   h->beam_done = false;
   return CASR_OK;
+}
+
+int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, int Tp, void* stream) {
+  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
+  if (!h->W) return fail(h, CASR_ERR_STATE, "casr_encode: no weights bound");
+  if (!feat || !lens || B <= 0 || Tp <= 0) return fail(h, CASR_ERR_ARG, "casr_encode: bad arguments");
+  HIP_OK(h, hipSetDevice(h->device));
+  return encode_impl(h, feat, lens, B, Tp, (hipStream_t)stream);
+}
+
+int casr_encode_fbank(casr_handle* h, const float* fbank, const int32_t* frames, int B, int T, float eps,
+                      int32_t* feat_len, void* stream) {
+  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
+  if (!h->W) return fail(h, CASR_ERR_STATE, "casr_encode_fbank: no weights bound");
+  if (!fbank || !frames || B <= 0 || T < 3)
+    return fail(h, CASR_ERR_ARG, "casr_encode_fbank: bad arguments (B=%d T=%d)", B, T);
+  HIP_OK(h, hipSetDevice(h->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int rc = encode_impl(h, nullptr, nullptr, B, T / 3, s, fbank, frames, T, eps);
+  if (rc == CASR_OK && feat_len)
+    HIP_OK(h, hipMemcpyAsync(feat_len, h->lens.p, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
+  return rc;
 }
 
 int casr_encoder_results(casr_handle* h, float* enc, float* h_final, float* c_final, float* keys,

@@ -167,6 +167,10 @@ hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nma
                           const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s);
 
 // features.hip
+// the layer-0 s16 row image straight from fbank (features_fused_kernel<true>, T / 3 <= 272)
+bool features_x16_supported(int T);
+hipError_t launch_features_x16(const float* fbank, const int32_t* frames, int B, int T, float eps,
+                               int32_t* feat_len, uint16_t* x16, int Kp, int32_t* err, hipStream_t s);
 hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int T, float eps,
                            float* feat, int32_t* feat_len, hipStream_t s);
 hipError_t launch_gather_utts(const float* const* ptrs, const int32_t* lens, int B, int Tp,

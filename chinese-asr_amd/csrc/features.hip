@@ -131,10 +131,17 @@ __global__ __launch_bounds__(256) void cmvn_kernel(float* __restrict__ feat,
 constexpr int FM = 16, FQ = 9 * FM, FPH = 4, FNJ = 68;  // FNJ x FPH >= Tp (T <= 816 frames)
 static_assert(F % FM == 0, "mel slabs tile the 80 mels");
 
+// X16: instead of the f32 rows, the layer-0 s16 row image of the encoder's input projection
+// ([B Tp][Kp/32][32 hi | 32 lo] halves, split16_word of the same f32 value, zero columns
+// 720..Kp-1), so the f32 features never reach HBM and split_rows_kernel does not run
+// (casr_encode_fbank); a finite value beyond the f16 range raises CASR_DEV_F16_RANGE as there.
+template <bool X16>
 __global__ __launch_bounds__(FQ * FPH) void features_fused_kernel(const float* __restrict__ fbank,
                                                                   const int32_t* __restrict__ frames, int T,
                                                                   int Tp, float eps, float* __restrict__ feat,
-                                                                  int32_t* __restrict__ feat_len) {
+                                                                  int32_t* __restrict__ feat_len,
+                                                                  uint16_t* __restrict__ x16, int Kp,
+                                                                  int32_t* __restrict__ err) {
   extern __shared__ float xs[];  // [nf][FM]
   __shared__ float part[FPH][FQ];
   __shared__ float stat[2][FQ];
@@ -200,11 +207,42 @@ __global__ __launch_bounds__(FQ * FPH) void features_fused_kernel(const float* _
     __syncthreads();
     den = stat[1][q];
   }
-  float* out = feat + (size_t)b * Tp * D + o;
+  if constexpr (X16) {
+    // lanes q and q ^ 1 hold adjacent columns o, o + 1 (o even: FQ, the mel slab and FM are
+    // even): the even lane stores both hi halves as one word, the odd lane both lo halves
+    const bool odd = q & 1;
+    uint32_t* xo = reinterpret_cast<uint32_t*>(x16 + (size_t)b * Tp * Kp * 2 + ((o & ~1) / 32) * 64 +
+                                               ((o & ~1) % 32) + (odd ? 32 : 0));
+    bool range_ok = true;
 #pragma unroll
-  for (int i = 0; i < FNJ; ++i) {
-    const int j = ph + FPH * i;
-    if (j < Tp) out[(size_t)j * D] = (j < lp && eps >= 0.f) ? (vals[i] - mean) / den : vals[i];
+    for (int i = 0; i < FNJ; ++i) {
+      const int j = ph + FPH * i;
+      if (j < Tp) {  // uniform over the lane pair (same time phase)
+        const float y = (j < lp && eps >= 0.f) ? (vals[i] - mean) / den : vals[i];
+        const uint32_t wv = split16_word(y);
+        const uint32_t pw = (uint32_t)dpp_i<DPP_XOR1>((int)wv);
+        xo[(size_t)j * Kp] = odd ? ((pw >> 16) | (wv & 0xFFFF0000u)) : ((wv & 0xFFFFu) | (pw << 16));
+        const float m = fabsf(y);
+        range_ok &= !(m >= 65520.f && m < INFINITY);
+      }
+    }
+    if (!range_ok) __hip_atomic_fetch_or(err, CASR_DEV_F16_RANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0) {  // the zero columns D..Kp-1 of every row of this utterance
+      const int npad = Kp - D;
+      for (int i = tid; i < Tp * npad; i += FQ * FPH) {
+        const int j = i / npad, col = D + i % npad;
+        uint16_t* zp = x16 + ((size_t)b * Tp + j) * Kp * 2 + (col / 32) * 64 + (col % 32);
+        zp[0] = 0;
+        zp[32] = 0;
+      }
+    }
+  } else {
+    float* out = feat + (size_t)b * Tp * D + o;
+#pragma unroll
+    for (int i = 0; i < FNJ; ++i) {
+      const int j = ph + FPH * i;
+      if (j < Tp) out[(size_t)j * D] = (j < lp && eps >= 0.f) ? (vals[i] - mean) / den : vals[i];
+    }
   }
 }
 
@@ -215,8 +253,8 @@ hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int
   // eps < 0: no CMVN (the stacked features get_log_mel returns, data.py:226-249)
   if (Tp <= FNJ * FPH) {
     const size_t shm = (size_t)T * FM * sizeof(float);
-    hipLaunchKernelGGL(features_fused_kernel, dim3(F / FM, B), dim3(FQ * FPH), shm, s, fbank, frames, T, Tp, eps,
-                       feat, feat_len);
+    hipLaunchKernelGGL(features_fused_kernel<false>, dim3(F / FM, B), dim3(FQ * FPH), shm, s, fbank, frames, T, Tp,
+                       eps, feat, feat_len, nullptr, 0, nullptr);
     return hipGetLastError();
   }
   // longer utterances: the two-pass kernels
@@ -224,6 +262,18 @@ hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int
                      feat_len);
   if (eps >= 0.f)
     hipLaunchKernelGGL(cmvn_kernel, dim3((D + 63) / 64, B), dim3(256), 0, s, feat, feat_len, Tp, eps);
+  return hipGetLastError();
+}
+
+bool features_x16_supported(int T) { return T / 3 > 0 && T / 3 <= FNJ * FPH; }
+
+hipError_t launch_features_x16(const float* fbank, const int32_t* frames, int B, int T, float eps,
+                               int32_t* feat_len, uint16_t* x16, int Kp, int32_t* err, hipStream_t s) {
+  const int Tp = T / 3;
+  if (B <= 0 || !features_x16_supported(T) || Kp < D || Kp % 32 != 0) return hipErrorInvalidValue;
+  const size_t shm = (size_t)T * FM * sizeof(float);
+  hipLaunchKernelGGL(features_fused_kernel<true>, dim3(F / FM, B), dim3(FQ * FPH), shm, s, fbank, frames, T, Tp, eps,
+                     nullptr, feat_len, x16, Kp, err);
   return hipGetLastError();
 }
 

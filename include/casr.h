@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CASR_API_VERSION 1
+#define CASR_API_VERSION 2
 #define CASR_MAX_LAYERS 8
 
 enum {
@@ -135,6 +135,14 @@ int casr_gather_utterances(casr_handle* h, const float* const* utt_ptrs, const i
  * .compute_key_value (attention.py:67-78).  feat [B][Tp][feat_dim], lens [B] (<= Tp).
  * Results stay in the handle for the following casr_greedy / casr_beam. */
 int casr_encode(casr_handle* h, const float* feat, const int32_t* lens, int B, int Tp, void* stream);
+
+/* casr_features + casr_encode in one call, from fbank [B][T][n_mels] (frames [B]): the parse()
+ * chain main.py:36-53 (stacking, deltas, CMVN with eps, then RNNEncoder.forward).  The features
+ * stay inside the handle: in s16x3 arithmetic the feature kernel writes the encoder's layer-0
+ * split-f16 row image directly, so the f32 features never reach HBM (results equal the two-call
+ * sequence bit for bit).  feat_len [B] = frames[b]/3 is also written when not NULL. */
+int casr_encode_fbank(casr_handle* h, const float* fbank, const int32_t* frames, int B, int T, float eps,
+                      int32_t* feat_len, void* stream);
 
 /* Copy of the encoder results (tests / EncoderOutput): enc [B][Tp][2H] (zeros past len),
  * h_final / c_final [B][2H] (last layer [fw || bw]), keys [B][A][Tp] (any may be NULL). */

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     assert declared == sorted(L.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.casr_api_version() == 1
+    assert lib.casr_api_version() == 2
 
 
 def test_create_without_gpu_or_bad_config_fails_loudly():

@@ -278,6 +278,26 @@ def _bench_batch(eng, B, T=800):
     return eng.features(fb, torch.full((B,), T, dtype=torch.int32, device=eng.device))
 
 
+def test_encode_fbank_equals_features_then_encode(eng):
+    """casr_encode_fbank (features kept inside the handle; s16x3: written straight as the
+    layer-0 split-f16 image) gives the two-call sequence's encoder results bit for bit, ragged
+    lengths included, and the same feature lengths."""
+    bind(eng, "peaked")
+    fb, fr = batch_fbank(FRAMES, eng.device)
+    feat, flen = eng.features(fb, fr)
+    eng.encode(feat, flen)
+    a = [x.cpu() for x in eng.encoder_results()]
+    ga = eng.greedy()["tokens"].cpu()
+    flen2 = eng.encode_fbank(fb, fr)
+    assert eng.device_flags() == 0
+    b = [x.cpu() for x in eng.encoder_results()]
+    gb = eng.greedy()["tokens"].cpu()
+    assert torch.equal(flen.cpu(), flen2.cpu())
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert torch.equal(ga, gb)
+
+
 def test_full_length_greedy_matches_oracle(eng):
     """T = 800 (T' = 266), bench weights (no EOS: all 40 steps), B = 24 vs the CPU oracle."""
     enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True, eos_bias=0.0)
