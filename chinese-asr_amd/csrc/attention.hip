@@ -124,6 +124,9 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     // branch-free: a slot past the group's last row gets v = 0 (its keys load is zero-filled and
     // q is padded), so it adds an exact zero and the real terms keep their order; rows j >= nk
     // compute on q = 0 and are never stored
+    // one fused multiply-add per term (torch multiplies, then sums in its own order: the score
+    // is within the attention tolerance either way; hipcc already contracted the former
+    // round-to-nearest intrinsic pairs into these FMAs)
     auto batch = [&](const float4 (&kv)[CH], int ab) {
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
@@ -131,10 +134,10 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 #pragma unroll
         for (int j = 0; j < KPB; ++j) {
           const float qa = qs[(ab + i) * KPB + j];
-          e4[j][0] = __fadd_rn(e4[j][0], __fmul_rn(tanh_fast(kv[i].x + qa), va));
-          e4[j][1] = __fadd_rn(e4[j][1], __fmul_rn(tanh_fast(kv[i].y + qa), va));
-          e4[j][2] = __fadd_rn(e4[j][2], __fmul_rn(tanh_fast(kv[i].z + qa), va));
-          e4[j][3] = __fadd_rn(e4[j][3], __fmul_rn(tanh_fast(kv[i].w + qa), va));
+          e4[j][0] = fmaf(tanh_fast(kv[i].x + qa), va, e4[j][0]);
+          e4[j][1] = fmaf(tanh_fast(kv[i].y + qa), va, e4[j][1]);
+          e4[j][2] = fmaf(tanh_fast(kv[i].z + qa), va, e4[j][2]);
+          e4[j][3] = fmaf(tanh_fast(kv[i].w + qa), va, e4[j][3]);
         }
       }
     };
@@ -285,10 +288,10 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     auto fma4 = [&](const float (&al)[KPB], const float4& v) {
 #pragma unroll
       for (int j = 0; j < KPB; ++j) {
-        acc[j][0] = __fadd_rn(acc[j][0], __fmul_rn(al[j], v.x));
-        acc[j][1] = __fadd_rn(acc[j][1], __fmul_rn(al[j], v.y));
-        acc[j][2] = __fadd_rn(acc[j][2], __fmul_rn(al[j], v.z));
-        acc[j][3] = __fadd_rn(acc[j][3], __fmul_rn(al[j], v.w));
+        acc[j][0] = fmaf(al[j], v.x, acc[j][0]);
+        acc[j][1] = fmaf(al[j], v.y, acc[j][1]);
+        acc[j][2] = fmaf(al[j], v.z, acc[j][2]);
+        acc[j][3] = fmaf(al[j], v.w, acc[j][3]);
       }
     };
     int t = tp;

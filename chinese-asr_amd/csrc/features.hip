@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void stack_kernel(const float* __restrict__ fb
       for (int k = 0; k < 9; ++k) {
         const int tt = t + k - 4;
         const float xv = (tt >= 0 && tt < nf) ? x[(size_t)tt * F + m] : 0.f;
-        v = __fadd_rn(v, __fmul_rn(w[k], xv));
+        v = fmaf(w[k], xv, v);  // fused, as oneDNN's conv2d (torch's tap order)
       }
     }
     out[o] = v;
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(FQ * FPH) void features_fused_kernel(const float* _
         for (int k = 0; k < 9; ++k) {
           const int tt = t + k - 4;
           const float xv = (tt >= 0 && tt < nf) ? xs[tt * FM + mm] : 0.f;
-          v = __fadd_rn(v, __fmul_rn(w[k], xv));
+          v = fmaf(w[k], xv, v);  // fused, as oneDNN's conv2d (torch's tap order)
         }
       }
       s += v;

@@ -28,6 +28,18 @@ constexpr int NFFT = 512, HOP = 160, WIN = 400, LPAD = (NFFT - WIN) / 2, NBIN = 
 constexpr int NC = NFFT / 2;  // complex FFT size
 constexpr int FPB = 4;        // frames per block (one per wave)
 
+// torch's elementwise steps, each rounded (no FMA contraction: hipcc's default would fuse them):
+// pre-emphasis x[t+1] - 0.97 x[t] (data.py:201-202), the window product, |X|^2 = re^2 + im^2
+// (data.py:220-221)
+CASR_DEV float preemph_win(float w, float x1, float x0, float pre) {
+#pragma clang fp contract(off)
+  return w * (x1 - pre * x0);
+}
+CASR_DEV float power2(float re, float im) {
+#pragma clang fp contract(off)
+  return re * re + im * im;
+}
+
 __device__ __forceinline__ int bitrev8(int x) { return (int)(__brev((unsigned)x) >> 24); }
 
 __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ wav,
@@ -55,9 +67,9 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
     const int m = lane + 64 * i, j0 = 2 * m, j1 = j0 + 1;
     float v0 = 0.f, v1 = 0.f;
     if (live && j0 >= LPAD && j0 < LPAD + WIN)
-      v0 = __fmul_rn(k->win[j0 - LPAD], __fsub_rn(x[j0 + 1], __fmul_rn(pre, x[j0])));
+      v0 = preemph_win(k->win[j0 - LPAD], x[j0 + 1], x[j0], pre);
     if (live && j1 >= LPAD && j1 < LPAD + WIN)
-      v1 = __fmul_rn(k->win[j1 - LPAD], __fsub_rn(x[j1 + 1], __fmul_rn(pre, x[j1])));
+      v1 = preemph_win(k->win[j1 - LPAD], x[j1 + 1], x[j1], pre);
     const int r = bitrev8(m);
     zr[w][r] = v0;
     zi[w][r] = v1;
@@ -89,7 +101,7 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
     const double orr = 0.5 * (zi1 - zi2), oi = -0.5 * (zr1 - zr2);
     const double c = k->tw512r[q], sn = k->tw512i[q];
     const float xr = (float)(er + (orr * c - oi * sn)), xi = (float)(ei + (orr * sn + oi * c));
-    pw[w][q] = __fadd_rn(__fmul_rn(xr, xr), __fmul_rn(xi, xi));
+    pw[w][q] = power2(xr, xi);
   }
   __syncthreads();
   if (f >= Tmax) return;
@@ -100,7 +112,7 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
       continue;
     }
     float acc = 0.f;
-    for (int q = k->lo[m]; q < k->hi[m]; ++q) acc = __fadd_rn(acc, __fmul_rn(pw[w][q], k->fb[q * F + m]));
+    for (int q = k->lo[m]; q < k->hi[m]; ++q) acc = fmaf(pw[w][q], k->fb[q * F + m], acc);  // matmul: fused
     o[m] = logf(acc == 0.f ? 1.1920928955078125e-07f : acc);
   }
 }
