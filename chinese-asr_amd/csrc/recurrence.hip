@@ -97,7 +97,8 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, uint16_t* __restrict__ x16, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
-    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg, int pre_wait, int pre_sleep) {
+    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg, int pre_wait, int pre_sleep,
+    int poll_gap) {
   constexpr int NW = RG * UW / 64;      // waves: 4 k-chunks x RG/16 row halves x UW/16 unit halves
   __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
@@ -207,6 +208,44 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       }
       for (int i = 0; i < pre_sleep; ++i) __builtin_amdgcn_s_sleep(1);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      if (poll_gap > 0) {
+        // two polls in flight per pass, the second poll_gap x 64 clocks after the first: a first
+        // poll that arrives before the group's last store costs the gap instead of a round trip.
+        // Measured on one box, rec ms per greedy batch (3 rounds, interleaved): one poll after
+        // sleep 6 3.13-3.19; sleep 2 + gap 4 3.07-3.11; sleep 1 + gap 3 3.07-3.11; sleep 0 +
+        // gap 3-5 3.11-3.16; no own-store wait + sleep 4 + gap 3 3.08-3.14.  Default sleep 2, gap 4.
+        for (uint32_t pass = 0;; ++pass) {
+          asm volatile("" ::: "memory");
+          u32x4 v2[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + i * 16, 0, 16 /* sc1 */);
+          __builtin_amdgcn_sched_barrier(0);
+          for (int i = 0; i < poll_gap; ++i) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v2[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + i * 16, 0, 16 /* sc1 */);
+          __builtin_amdgcn_sched_barrier(0);
+          uint32_t bad = 0, bad2 = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bad |= (v[i].x ^ want) | (v[i].y ^ want) | (v[i].z ^ want) | (v[i].w ^ want);
+          npass = 2 * pass + 1;
+          if (__all((bad & TAG_BIT) == 0)) break;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bad2 |= (v2[i].x ^ want) | (v2[i].y ^ want) | (v2[i].z ^ want) | (v2[i].w ^ want);
+          npass = 2 * pass + 2;
+          if (__all((bad2 & TAG_BIT) == 0)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = v2[i];
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || pass > (1u << 21)) {
+            if (lane == 0) {
+              s_quit[s & 1] = 1;
+              __hip_atomic_fetch_or(err, CASR_DEV_REC_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+          }
+        }
+      } else
       for (uint32_t pass = 0;; ++pass) {
         asm volatile("" ::: "memory");
         uint32_t bad = 0;
@@ -368,7 +407,11 @@ static int rec_pre_wait() {
   return v;
 }
 static int rec_pre_sleep() {
-  static const int v = env_int("CASR_REC_PRESLEEP", 6);
+  static const int v = env_int("CASR_REC_PRESLEEP", 2);
+  return v;
+}
+static int rec_poll_gap() {
+  static const int v = env_int("CASR_REC_POLLGAP", 4);  // 0: one poll per pass
   return v;
 }
 
@@ -430,7 +473,7 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
   dim3 grid((H / UW) * nrg * 2);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(RG * UW), 0, s, Whh_f, Gin, xin, out, x16, hx, hfin, cst, lens, B, Bp, Tp,
-                       residual, err, trace, nrg, rec_pre_wait(), rec_pre_sleep());
+                       residual, err, trace, nrg, rec_pre_wait(), rec_pre_sleep(), rec_poll_gap());
   };
   switch (rec_layout()) {
     case 1: s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>); break;
