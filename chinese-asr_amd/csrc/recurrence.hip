@@ -13,7 +13,8 @@
 //   o * tanh(c) has |h| <= 1, so bit 30 (the exponent MSB, set only for |x| >= 2) is always
 //   0 in a finite h and is free to carry the tag; a non-finite h is sent as 0x3FFFFFFF (a
 //   value in [1, 2) no LSTM output takes) and decoded back to NaN.  Producers store each word
-//   write-through (sc1); a consumer wave re-reads (sc1 loads, L1 bypassed) its 16 rows x 64
+//   write-through (sc1), or plain when its whole group shares its XCD (see the placement table
+//   below); a consumer wave re-reads (sc1 loads, L1 bypassed) its 16 rows x 64
 //   units until every tag matches: no counter, no fence, no barrier, 4 B per value.
 //
 // Geometry (gfx950, 256 CUs): workgroup (ub, rg, d) = 16 hidden units (64 gate rows, all four
@@ -52,7 +53,7 @@ constexpr uint32_t NONFINITE = 0x3FFFFFFFu;
 // travels as hi = f16(h) (NaN) with lo = 0.  The consumer masks the tag and feeds the halves to
 // the f16 MFMAs directly.
 template <bool S16>
-CASR_DEV void store_granule(uint32_t* p, int step_tagged, float v) {
+CASR_DEV void store_granule(uint32_t* p, int step_tagged, float v, int plain) {
   uint32_t x;
   if constexpr (S16) {
     x = split16_word(v);
@@ -61,7 +62,10 @@ CASR_DEV void store_granule(uint32_t* p, int step_tagged, float v) {
     if (!(fabsf(v) < 2.0f)) x = NONFINITE;
   }
   x |= (step_tagged & 1) ? TAG_BIT : 0u;
-  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dword sc1
+  if (plain)
+    __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // global_store_dword
+  else
+    __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dword sc1
 }
 
 // s_waitcnt vmcnt(min(n, 7)) (expcnt / lgkmcnt untouched): the count is an immediate, n is
@@ -98,7 +102,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     float* __restrict__ out, uint16_t* __restrict__ x16, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
     int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg, int pre_wait, int pre_sleep,
-    int poll_gap) {
+    int poll_gap, int store_plain) {
   constexpr int NW = RG * UW / 64;      // waves: 4 k-chunks x RG/16 row halves x UW/16 unit halves
   __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
@@ -130,11 +134,42 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   const size_t si = ((size_t)d * B + b) * H + U;       // hfin / cst index (valid when b < B)
   const size_t gi = ((size_t)d * Bp + b) * H + U;      // granule index within a buffer
   const int x16_col = ((d * H + U) >> 5) * 64 + ((d * H + U) & 31);  // s16 image column of (d, U)
+  __shared__ int s_plain;
   if (tid == 0) {
     s_tmax = 0;
     s_quit[0] = s_quit[1] = 0;
   }
+  // ---- hand-off store flavour (speed only, never correctness).  A plain (sc0) store keeps the
+  // word's line in this XCD's L2, where a same-XCD member's sc1 poll (L1 bypassed, L2-served)
+  // finds it without the memory-side round trip an sc1 store (line dropped from L2) costs; a
+  // member on another XCD would never see it (MI355X_MICROARCH.md, stores of each flavour).  So
+  // each workgroup publishes its XCC id (sc1) in a per-launch table (zeroed by reset_rec_layer)
+  // and stores plain only when it has read all P ids of its group equal to its own: every
+  // consumer of its words is then on its XCD.  Any other outcome (another XCD, a poll bound)
+  // keeps sc1 stores, which every consumer sees wherever it runs.
+  if (w == 0) {
+    int plain = 0;
+    if (store_plain) {
+      uint32_t* xt = hx + (size_t)3 * 2 * plane;
+      uint32_t xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+      const uint32_t me = 0x100u | (xcc & 0xFu);
+      if (lane == 0) __hip_atomic_store(xt + grp * P + mem, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t got = me;
+      if (lane < P) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+          got = __hip_atomic_load(xt + grp * P + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((got & 0x100u) || __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS / 1000) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      plain = __all(got == me) ? 1 : 0;
+    }
+    if (lane == 0) s_plain = plain;
+  }
   __syncthreads();
+  const int plain_st = s_plain;
   if (u == 0 && len > 0) atomicMax(&s_tmax, len);
 
   // ---- this wave's W_hh fragments, resident for the whole layer (64 VGPRs)
@@ -198,7 +233,8 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       // trip.  Measured (ms per greedy batch): no wait 5.95, wait + sleep 0 / 2 / 4 / 5 / 6 / 8 /
       // 10 = 3.05 / 3.24 / 2.91 / 2.80 / 2.82-2.85 / 2.87 / 2.89; wait + 6.  With the layer
       // outputs stored after the hand-off word, waiting for the word alone (default 2) measured
-      // 8.29 vs 8.33 ms greedy, 9.33-9.36 vs 9.46 ms beam.
+      // 8.29 vs 8.33 ms greedy, 9.33-9.36 vs 9.46 ms beam.  Those numbers predate the plain
+      // hand-off stores and the two-poll passes below, with which the default is no wait.
       // pre_wait 2: wait for the hand-off word only, not for the vector-memory operations this
       // wave issued after it (n_after, counted by the previous step from what it actually issued)
       if (pre_wait == 2) {
@@ -213,7 +249,9 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
         // poll that arrives before the group's last store costs the gap instead of a round trip.
         // Measured on one box, rec ms per greedy batch (3 rounds, interleaved): one poll after
         // sleep 6 3.13-3.19; sleep 2 + gap 4 3.07-3.11; sleep 1 + gap 3 3.07-3.11; sleep 0 +
-        // gap 3-5 3.11-3.16; no own-store wait + sleep 4 + gap 3 3.08-3.14.  Default sleep 2, gap 4.
+        // gap 3-5 3.11-3.16; no own-store wait + sleep 4 + gap 3 3.08-3.14.  With plain (L2-kept)
+        // hand-off stores (below): wait 2 + sleep 0 + gap 2 2.83-2.88, no wait + sleep 0 / 1 / 2 +
+        // gap 2 2.78-2.87 / 2.80-2.82 / 2.80-2.86, gap 1 2.82-2.87.  Default: no wait, sleep 1, gap 2.
         for (uint32_t pass = 0;; ++pass) {
           asm volatile("" ::: "memory");
           u32x4 v2[4];
@@ -341,7 +379,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     }
     if (quit) return false;
     // the hand-off word goes out first: the layer outputs below are off the step chain
-    if (s + 1 < tmax) store_granule<S16>(hx + (size_t)((s + 1) % 3) * 2 * plane + gi, s + 1, h2);
+    if (s + 1 < tmax) store_granule<S16>(hx + (size_t)((s + 1) % 3) * 2 * plane + gi, s + 1, h2, plain_st);
     if (act) {
       const int t = (d == 0) ? s : (len - 1 - s);
       const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
@@ -403,15 +441,17 @@ static int env_int(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 static int rec_pre_wait() {
-  static const int v = env_int("CASR_REC_PREWAIT", 2);  // 0 none, 1 vmcnt(0), 2 hand-off word only
+  static const int v = env_int("CASR_REC_PREWAIT", 0);  // 0 none, 1 vmcnt(0), 2 hand-off word only
   return v;
 }
 static int rec_pre_sleep() {
-  static const int v = env_int("CASR_REC_PRESLEEP", 2);
+  static const int v = env_int("CASR_REC_PRESLEEP", 1);
   return v;
 }
+// read at every launch (not cached) so a test can compare both hand-off store flavours in one process
+static int rec_store_plain() { return env_int("CASR_REC_STOREPLAIN", 1); }
 static int rec_poll_gap() {
-  static const int v = env_int("CASR_REC_POLLGAP", 4);  // 0: one poll per pass
+  static const int v = env_int("CASR_REC_POLLGAP", 2);  // 0: one poll per pass
   return v;
 }
 
@@ -427,9 +467,11 @@ static int rec_layout() {
 static int rec_rows() { return rec_layout() == 0 ? 32 : 16; }
 static int rec_units() { return rec_layout() == 1 ? 32 : 16; }
 
+// the three granule buffers, then the placement table (one word per workgroup)
+static size_t rec_granule_words(int B) { return (size_t)3 * 2 * ((B + 31) / 32 * 32) * H; }
+
 size_t rec_layer_granule_bytes(int B) {
-  const int Bp = (B + 31) / 32 * 32;
-  return (size_t)3 * 2 * Bp * H * sizeof(uint32_t);
+  return (rec_granule_words(B) + (size_t)rec_layer_grid_blocks(B)) * sizeof(uint32_t);
 }
 
 int rec_layer_waves() { return rec_rows() * rec_units() / 64; }
@@ -459,9 +501,11 @@ hipError_t rec_layer_occupancy(int* blocks_per_cu) {
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
   // Guideline 16: re-initialise every call.  Buffer j is first read at step j (j = 1, 2) or 3
   // (j = 0), expecting parity 1, 0, 1: fill buffers 0 and 1 with parity 0, buffer 2 with 1.
-  const size_t per = rec_layer_granule_bytes(B) / 4 / 3;
+  // The placement table after them starts at 0 (no id published).
+  const size_t per = rec_granule_words(B) / 3;
   hipError_t e = fill_u32(hx, 0u, 2 * per, s);
-  return e == hipSuccess ? fill_u32(hx + 2 * per, TAG_BIT, per, s) : e;
+  if (e == hipSuccess) e = fill_u32(hx + 2 * per, TAG_BIT, per, s);
+  return e == hipSuccess ? fill_u32(hx + 3 * per, 0u, (size_t)rec_layer_grid_blocks(B), s) : e;
 }
 
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
@@ -473,7 +517,8 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
   dim3 grid((H / UW) * nrg * 2);
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(RG * UW), 0, s, Whh_f, Gin, xin, out, x16, hx, hfin, cst, lens, B, Bp, Tp,
-                       residual, err, trace, nrg, rec_pre_wait(), rec_pre_sleep(), rec_poll_gap());
+                       residual, err, trace, nrg, rec_pre_wait(), rec_pre_sleep(), rec_poll_gap(),
+                       rec_store_plain());
   };
   switch (rec_layout()) {
     case 1: s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>); break;

@@ -7,6 +7,8 @@ chain's) and libm ulps):
   features 2e-5 abs, encoder outputs 1e-4 abs, beam / greedy scores 2e-3 abs (sums of up to
   40 log-probs of magnitude <= ~40), attention weights 1e-5 abs; token ids must be identical.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -219,8 +221,8 @@ def test_graph_replay_equals_eager(eng):
 
 @pytest.mark.parametrize("B", [37, 256])
 def test_persistent_recurrence_equals_per_step(eng, B):
-    """The persistent per-layer recurrence (granule hand-offs) and the per-step launches give
-    bitwise-identical encoder outputs and final states, on ragged lengths (B = 37: a partial
+    """The persistent per-layer recurrence (granule hand-offs, either store flavour) and the
+    per-step launches give bitwise-identical encoder outputs and final states, on ragged lengths (B = 37: a partial
     32-row group and padding rows; B = 256: the full 256-workgroup grid)."""
     enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
     eng.bind(pack_weights(CFG, enc_sd, dec_sd))
@@ -234,12 +236,18 @@ def test_persistent_recurrence_equals_per_step(eng, B):
                               torch.from_numpy(frames.astype(np.int32)).to(eng.device))
     assert eng.recurrence_mode(B) == 1, "B <= 256 must take the persistent path on MI355X"
     outs = []
-    for persistent in (False, True, True):
-        eng.set_persistent(persistent)
-        eng.encode(feat, flen)
-        assert eng.device_flags() == 0
-        outs.append([t.cpu() for t in eng.encoder_results()])
-    eng.set_persistent(True)
+    # the persistent path twice: hand-off words stored plain (L2-kept, the default when each
+    # group shares an XCD) and write-through (CASR_REC_STOREPLAIN=0, read at every launch)
+    try:
+        for persistent, plain in ((False, "1"), (True, "1"), (True, "0")):
+            os.environ["CASR_REC_STOREPLAIN"] = plain
+            eng.set_persistent(persistent)
+            eng.encode(feat, flen)
+            assert eng.device_flags() == 0
+            outs.append([t.cpu() for t in eng.encoder_results()])
+    finally:
+        os.environ.pop("CASR_REC_STOREPLAIN", None)
+        eng.set_persistent(True)
     for ref, got in ((outs[0], outs[1]), (outs[1], outs[2])):
         for a, b in zip(ref, got):
             assert torch.equal(a, b)
