@@ -41,6 +41,8 @@ def build(force=False, verbose=False):
     os.makedirs(objdir, exist_ok=True)
     common = [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall",
               "-Wno-unused-result", f"-I{INCLUDE}", f"-I{CSRC}"]
+    # diagnostic builds only (ablation macros such as -DCASR_DG_DIAG=1; never the shipped library)
+    common += os.environ.get("CASR_EXTRA_FLAGS", "").split()
     procs, objs = [], []
     for src in sources():
         obj = os.path.join(objdir, os.path.basename(src)[:-4] + ".o")

@@ -56,6 +56,9 @@ namespace casr {
 // NR row blocks of one weight column slice get ids with the same L % 8: the slice is fetched into
 // one XCD's L2 once and re-read from there by every row block.
 constexpr int DG_BK = 64;
+#ifndef CASR_DG_DIAG
+#define CASR_DG_DIAG 0
+#endif
 
 __device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
   const int L = blockIdx.x, x = L & 7, j = L >> 3;
@@ -103,10 +106,16 @@ __device__ __forceinline__ void static_for(F&& f) {
 // (two swizzled 16-B chunks) and W block [j][hi|lo][lane].
 // ntiles: 16-row W fragment blocks that exist; a block's tiles past it re-read the last one (their
 // columns are discarded by the epilogue).
-template <int WR, int NT, int S, class ASrc, class Epi, bool S16 = false>
+// RS, WC (beam shapes): each wave multiplies RS 16-row slabs (so every W fragment it reads from
+// LDS feeds RS MFMA rows) by NT / WC of the block's column tiles; KQ = 8 / (WR WC) k slices.
+// IL (s16): the next tile's DMA slots are issued between this tile's MFMA groups (one per column
+// tile of the wave's first k-step) instead of in one burst after the barrier.
+template <int WR, int NT, int S, class ASrc, class Epi, bool S16 = false, int RS = 1, int WC = 1, bool IL = false>
 __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntiles, int nkt,
                                                     const float* __restrict__ Wf, ASrc asrc, Epi epi) {
-  constexpr int KQ = 8 / WR, QPW = 4 / KQ, BM = 16 * WR, ATILE = BM * DG_BK, WTILE = NT * FRAG;
+  constexpr int KQ = 8 / (WR * WC), QPW = 4 / KQ, BM = 16 * WR * RS, NTW = NT / WC;
+  static_assert(WR * WC * KQ == 8 && NT % WC == 0 && KQ <= 4, "8 waves = row groups x column groups x k slices");
+  constexpr int ATILE = BM * DG_BK, WTILE = NT * FRAG;
   constexpr int STG = ATILE + WTILE;          // floats per stage: [A tile | W tile]
   constexpr int NA = BM / 4, NDMA = NA + 4 * NT;  // DMA instructions per stage: A (4 rows each) + W
   constexpr int NSLOT = (NDMA + 7) / 8;      // per wave (at most)
@@ -129,7 +138,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   };
   int nb, rb;
   if (!xcd_tile(NB, NR, nb, rb)) return;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ws = w % WR, kq = w / WR;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ws = w % WR, wc = (w / WR) % WC, kq = w / (WR * WC);
   uint32_t* dtr = g_dg_trace ? g_dg_trace + ((size_t)Epi::kTraceClass * 4096 + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int i) {
     if (dtr && tid == 0) dtr[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -155,12 +164,12 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       wsrc[j] = Wf + (size_t)t * nkt * FRAG + qq * 256 + lane * 4;
     }
   }
-  auto stage = [&](float* dst, int kt) {
-    float* la = dst;
-    float* lw = dst + ATILE;
-    const int k0 = kt * DG_BK;
-#pragma unroll
-    for (int j = 0; j < NSLOT; ++j) {
+  auto stage_slot = [&](float* dst, int kt, auto J) {
+    constexpr int j = decltype(J)::value;
+    if constexpr (j < NSLOT) {
+      float* la = dst;
+      float* lw = dst + ATILE;
+      const int k0 = kt * DG_BK;
       const int i = w + 8 * j;
       if (i < NA) {
         const int row = 4 * i + (lane >> 4), c = (lane & 15) ^ (row & 15);
@@ -172,46 +181,73 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       }
     }
   };
+  auto stage = [&](float* dst, int kt) { static_for<0, NSLOT>([&](auto J) { stage_slot(dst, kt, J); }); };
+  constexpr bool ILS = IL && S16;
 
-  f32x4 acc[NT], accx[NT];
+  f32x4 acc[RS][NTW], accx[RS][NTW];
 #pragma unroll
-  for (int tn = 0; tn < NT; ++tn) acc[tn] = accx[tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int arow = ws * 16 + r;
-  auto compute = [&](const float* src, int kt) {
+  for (int rs = 0; rs < RS; ++rs)
+#pragma unroll
+    for (int tn = 0; tn < NTW; ++tn) acc[rs][tn] = accx[rs][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto arow = [&](int rs) { return (ws * RS + rs) * 16 + r; };
+  auto compute = [&](const float* src, int kt, auto&& issue) {
     const float* la = src;
-    const float* lw = src + ATILE;
+    const float* lw = src + ATILE + wc * NTW * FRAG;
     if constexpr (S16) {
+      bool pend = ILS;  // DMA slots of the next tile not issued yet (wave-uniform)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         if ((2 * kt + j) % KQ != kq) continue;
         const int c0 = 4 * g + 2 * j;
-        const u32x4 w0 = *reinterpret_cast<const u32x4*>(la + arow * DG_BK + ((c0 ^ (arow & 15)) << 2));
-        const u32x4 w1 = *reinterpret_cast<const u32x4*>(la + arow * DG_BK + (((c0 + 1) ^ (arow & 15)) << 2));
-        f16x8 ah, al;
-        unpack16(w0, w1, ah, al);
+        f16x8 ah[RS], al[RS];
 #pragma unroll
-        for (int tn = 0; tn < NT; ++tn) {
+        for (int rs = 0; rs < RS; ++rs) {
+          const int ar = arow(rs);
+          const u32x4 w0 = *reinterpret_cast<const u32x4*>(la + ar * DG_BK + ((c0 ^ (ar & 15)) << 2));
+          const u32x4 w1 = *reinterpret_cast<const u32x4*>(la + ar * DG_BK + (((c0 + 1) ^ (ar & 15)) << 2));
+          unpack16(w0, w1, ah[rs], al[rs]);
+        }
+        static_for<0, NTW>([&](auto TN) {
+          constexpr int tn = decltype(TN)::value;
           const f16x8 bh = *reinterpret_cast<const f16x8*>(lw + tn * FRAG + (2 * j) * 256 + lane * 4);
           const f16x8 bl = *reinterpret_cast<const f16x8*>(lw + tn * FRAG + (2 * j + 1) * 256 + lane * 4);
-          mfma_s16(ah, al, bh, bl, acc[tn], accx[tn]);
+#pragma unroll
+          for (int rs = 0; rs < RS; ++rs) mfma_s16(ah[rs], al[rs], bh, bl, acc[rs][tn], accx[rs][tn]);
+          if constexpr (ILS) {
+            if (pend) issue(TN);
+          }
+        });
+        if constexpr (ILS) {
+          if (pend) static_for<NTW, NSLOT>(issue);
+          pend = false;
         }
+      }
+      if constexpr (ILS) {
+        if (pend) static_for<0, NSLOT>(issue);  // no k-step of this tile is this wave's
       }
       return;
     }
 #pragma unroll
     for (int qh = 0; qh < QPW; ++qh) {
       const int q = kq * QPW + qh;
-      const float4 a = *reinterpret_cast<const float4*>(la + arow * DG_BK + (((4 * g + q) ^ (arow & 15)) << 2));
-      float4 b[NT];
+      float4 a[RS];
 #pragma unroll
-      for (int tn = 0; tn < NT; ++tn) b[tn] = *reinterpret_cast<const float4*>(lw + tn * FRAG + q * 256 + lane * 4);
-#pragma unroll
-      for (int tn = 0; tn < NT; ++tn) {
-        acc[tn] = mfma16x16x4(a.x, b[tn].x, acc[tn]);
-        acc[tn] = mfma16x16x4(a.y, b[tn].y, acc[tn]);
-        acc[tn] = mfma16x16x4(a.z, b[tn].z, acc[tn]);
-        acc[tn] = mfma16x16x4(a.w, b[tn].w, acc[tn]);
+      for (int rs = 0; rs < RS; ++rs) {
+        const int ar = arow(rs);
+        a[rs] = *reinterpret_cast<const float4*>(la + ar * DG_BK + (((4 * g + q) ^ (ar & 15)) << 2));
       }
+      float4 b[NTW];
+#pragma unroll
+      for (int tn = 0; tn < NTW; ++tn) b[tn] = *reinterpret_cast<const float4*>(lw + tn * FRAG + q * 256 + lane * 4);
+#pragma unroll
+      for (int rs = 0; rs < RS; ++rs)
+#pragma unroll
+        for (int tn = 0; tn < NTW; ++tn) {
+          acc[rs][tn] = mfma16x16x4(a[rs].x, b[tn].x, acc[rs][tn]);
+          acc[rs][tn] = mfma16x16x4(a[rs].y, b[tn].y, acc[rs][tn]);
+          acc[rs][tn] = mfma16x16x4(a[rs].z, b[tn].z, acc[rs][tn]);
+          acc[rs][tn] = mfma16x16x4(a[rs].w, b[tn].w, acc[rs][tn]);
+        }
     }
   };
 
@@ -221,9 +257,12 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   // after the first ring stages are in flight: the epilogue's operands (bias, predecessor rows,
   // W_hidden), loaded under the k loop, and the early-exit check (its wait also retires those
   // stages: a skipped block leaves no DMA behind)
-  const int erow0 = rb * BM + ws * 16 + 4 * (lane >> 4);
-  typename Epi::Pre pre;
-  if (kq == 0) epi.template prefetch<NT>(pre, erow0, nb, lane & 15, bad);
+  auto erow0 = [&](int rs) { return rb * BM + (ws * RS + rs) * 16 + 4 * (lane >> 4); };
+  const int nbw = nb * WC + wc;  // the wave's column block in units of NTW tiles (the epilogue's nb)
+  typename Epi::Pre pre[RS];
+  if (kq == 0)
+#pragma unroll
+    for (int rs = 0; rs < RS; ++rs) epi.template prefetch<NTW>(pre[rs], erow0(rs), nbw, lane & 15, bad);
   if (epi.skip()) return;
   if (bad) atomicOr(epi.err_flags(), bad);
   stamp(1);
@@ -237,54 +276,73 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of tile kt-1 are done
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");  // no LDS read of tile kt moves above the barrier
-      if (kt + S - 1 < nkt) stage(buf(std::integral_constant<int, (I + S - 1) % S>{}), kt + S - 1);
+      // CASR_DG_DIAG (diagnostic builds, tools/probes): bit 0 drops the k loop's DMA, bit 1 the MFMAs
+      auto issue = [&](auto J) {
+        if (kt + S - 1 < nkt && !(CASR_DG_DIAG & 1))
+          stage_slot(buf(std::integral_constant<int, (I + S - 1) % S>{}), kt + S - 1, J);
+      };
+      if constexpr (!ILS) static_for<0, NSLOT>(issue);
       if (kt == 0) stamp(2);
-      compute(buf(I), kt);
+      if (!(CASR_DG_DIAG & 2)) compute(buf(I), kt, issue);
+      else if constexpr (ILS) static_for<0, NSLOT>(issue);
     });
   }
   __syncthreads();  // nothing in flight any more: every wave is done reading the ring
   stamp(3);
-  if (kq == 0) epi.late(pre, erow0, nb, lane & 15);  // dependent loads, under the k-slice exchange
+  if (kq == 0)
+#pragma unroll
+    for (int rs = 0; rs < RS; ++rs) epi.late(pre[rs], erow0(rs), nbw, lane & 15);  // under the k-slice exchange
   if constexpr (S16) {
 #pragma unroll
-    for (int tn = 0; tn < NT; ++tn)
+    for (int rs = 0; rs < RS; ++rs)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[tn][e] = s16_combine(acc[tn][e], accx[tn][e]);
+      for (int tn = 0; tn < NTW; ++tn)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[rs][tn][e] = s16_combine(acc[rs][tn][e], accx[rs][tn][e]);
   }
   // k slices 1..KQ-1 hand their partial sums to slice 0 through LDS (the ring is free now)
   if constexpr (KQ > 1) {
     f32x4* part = reinterpret_cast<f32x4*>(lb0);
-    static_assert((KQ - 1) * WR * NT * 64 * 16 <= STG * 4, "partials fit one stage buffer");
+    static_assert((KQ - 1) * WR * WC * RS * NTW * 64 * 16 <= STG * 4, "partials fit one stage buffer");
+    auto slot = [&](int j, int rs, int tn) { return ((((j * WR + ws) * WC + wc) * RS + rs) * NTW + tn) * 64 + lane; };
     if (kq > 0) {
 #pragma unroll
-      for (int tn = 0; tn < NT; ++tn) part[(((kq - 1) * WR + ws) * NT + tn) * 64 + lane] = acc[tn];
+      for (int rs = 0; rs < RS; ++rs)
+#pragma unroll
+        for (int tn = 0; tn < NTW; ++tn) part[slot(kq - 1, rs, tn)] = acc[rs][tn];
     }
     __syncthreads();
     if (kq > 0) return;
 #pragma unroll
     for (int j = 0; j < KQ - 1; ++j)
 #pragma unroll
-      for (int tn = 0; tn < NT; ++tn) acc[tn] += part[((j * WR + ws) * NT + tn) * 64 + lane];
+      for (int rs = 0; rs < RS; ++rs)
+#pragma unroll
+        for (int tn = 0; tn < NTW; ++tn) acc[rs][tn] += part[slot(j, rs, tn)];
   }
-  // lane holds rows rb*BM + ws*16 + 4g + e (e = 0..3), column (nb*NT + tn)*16 + r
+  // lane holds rows erow0(rs) + e (e = 0..3), column (nbw*NTW + tn)*16 + r
   // per-wave LDS scratch for the epilogue (ring buffers are free now; the k-slice exchange
-  // above used lb0, and waves with ws < 4 take lb1): 16 rows x (16 NT + 4) floats
-  static_assert(4 * 16 * (16 * NT + 4) <= STG, "epilogue slabs fit a stage buffer");
-  float* escr = (ws < 4 ? lb1 : lb0) + (ws & 3) * 16 * (16 * NT + 4);
-  epi.template run<NT>(acc, erow0, nb, r, pre, escr);
+  // above used lb0 (only when KQ > 1, i.e. at most 4 epilogue waves, all on lb1)): 16 rows x
+  // (16 NTW + 4) floats per epilogue wave, reused by its RS slabs in turn (LDS is in order per wave)
+  static_assert(4 * 16 * (16 * NTW + 4) <= STG, "epilogue slabs fit a stage buffer");
+  const int ew = ws * WC + wc;
+  float* escr = (ew < 4 ? lb1 : lb0) + (ew & 3) * 16 * (16 * NTW + 4);
+#pragma unroll
+  for (int rs = 0; rs < RS; ++rs) epi.template run<NTW>(acc[rs], erow0(rs), nbw, r, pre[rs], escr);
   stamp(4);
 }
 
-template <int WR, int NT, int S, class ASrc, class Epi>
+template <int WR, int NT, int S, int RS = 1, int WC = 1, bool IL = false, class ASrc, class Epi>
 static void launch_dg(int NB, int R, int ntiles, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi,
                       int s16, hipStream_t s) {
-  const int NR = (R + 16 * WR - 1) / (16 * WR);
+  constexpr int BM = 16 * WR * RS;
+  const int NR = (R + BM - 1) / BM;
   if (s16)
-    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s, NB, NR,
-                       ntiles, nkt, Wf, asrc, epi);
+    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s,
+                       NB, NR, ntiles, nkt, Wf, asrc, epi);
   else
-    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, false>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s, NB,
-                       NR, ntiles, nkt, Wf, asrc, epi);
+    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, false, RS, WC>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s,
+                       NB, NR, ntiles, nkt, Wf, asrc, epi);
 }
 
 // A rows of the decoder LSTM: [embed(tok[r]) | st_old[src[r]][0:1024] = ctx | h]; a 64-deep
@@ -1306,7 +1364,16 @@ __global__ void beam_records_kernel(int B, int k, int L, const int32_t* __restri
 //   LSTMCell (N = 2048, 16 units x 4 gates per block): R <= 256: 32 rows, ring 4; R <= 512:
 //   64 rows, ring 4; else 128 rows, ring 3.
 //   projection (N = 5056 = 316 16-column tiles): R <= 256: 64 rows x 80 columns, ring 4;
-//   else 128 x 80, ring 3 (<= 156 KB of LDS each).
+//   R <= 512: 128 x 80, ring 3 (<= 156 KB of LDS each); else 128 x 160, ring 2, each wave 32 rows
+//   (RS = 2: every W fragment it reads feeds two MFMA row slabs) x 80 columns (WC = 2).
+// At R > 512 (beam) both GEMMs issue the next tile's DMA between their MFMA groups (IL).
+// Beam ablations at R = 1024 (k loop per block, us; tools/probes/dg_diag.sh): projection 27.9
+// full, 19.8 without the k loop's DMA, 13.8 without its MFMAs; LSTMCell 18.6 / 13.0 / 7.1.  The
+// compute phase (s16x3: 3 MFMAs per product) and the DMA overlapped poorly: all 8 waves issued
+// their 9 DMA instructions in one burst after each barrier, with the MFMA pipes idle.  Interleaved
+// (A/B, ms per beam batch): projection 1.75 -> 1.67, with the 32 x 80 wave tiles 1.61; LSTMCell
+// 1.27 -> 1.24.  The greedy shapes (R = 256, 2-3 DMA instructions per wave and tile) measured
+// slower interleaved (0.82 -> 0.86-0.88 ms each) and keep the burst.
 // Measured at R = 256 (bench, ms per greedy batch of 40 steps): projection 64 x 80 ring 4 0.88
 // against 1.11 for the 32 x 64 two-buffer tile of 640 blocks, 1.19 for 64 x 64 ring 4 (316
 // blocks), 1.59 for 32 x 64 ring 6 (LDS then admits one of its 2.5 blocks per CU); the LSTMCell
@@ -1317,7 +1384,7 @@ static void launch_dec_lstm(int R, const float* Wf, const ASrc& asrc, const Epi&
   const int NB = HD / 16, ntiles = 4 * NB, nkt = KDEC / DG_BK;
   if (R <= 256) launch_dg<2, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 512) launch_dg<4, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  else launch_dg<8, 4, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else launch_dg<8, 4, 3, 1, 1, true>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
 template <class ASrc, class Epi>
@@ -1326,15 +1393,15 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
   const int nkt = KPROJ / DG_BK, NB = (ntiles + 4) / 5;  // 5 column tiles per block (10 at R > 512)
   if (R <= 256) launch_dg<4, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 512) launch_dg<8, 5, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  else launch_dg<8, 10, 2>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else launch_dg<4, 10, 2, 2, 2, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
 // ------------------------------------------------------------------ host drivers
 // per-block row partials from the projection epilogue: the vocabulary must fit the 64 partial
 // blocks; beam search uses them at temperature 1 only (they are of x, not x / T)
 static int proj_col_blocks(const DecodeArgs& a) {
-  const int R = a.B * a.k, nt = a.L.VP / 16;
-  return R > 512 ? (nt + 9) / 10 : (nt + 4) / 5;
+  const int nt = a.L.VP / 16;
+  return (nt + 4) / 5;  // 5-tile column blocks (at R > 512: two per 10-tile block, one per wave column)
 }
 static bool row_partials(const DecodeArgs& a) {
   return proj_col_blocks(a) <= GP_NB && (a.greedy_run || a.temperature == 1.0f);

@@ -1,5 +1,6 @@
 """One warm greedy step at the headline config (B=256, T=800) for PMC collection (rocprofv3
---pmc passes); runs the same launches as one bench.py step."""
+--pmc passes); runs the same launches as one bench.py step.  BEAM=k: a beam step instead (set B
+too, e.g. B=128 BEAM=8 for the bench's beam line)."""
 import os
 import sys
 
@@ -21,6 +22,9 @@ frames = torch.full((B,), T, dtype=torch.int32, device="cuda")
 for _ in range(int(os.environ.get("STEPS", 2))):
     feat, flen = eng.features(fb, frames)
     eng.encode(feat, flen)
-    eng.greedy()["tokens"].cpu()
+    if int(os.environ.get("BEAM", 0)):
+        eng.beam(int(os.environ["BEAM"]))
+    else:
+        eng.greedy()["tokens"].cpu()
 torch.cuda.synchronize()
 print("ok")
