@@ -22,6 +22,8 @@
 // row r at c ^ ((r >> 1) & 7).  Grid: XCD-aware tile order (encoder.hip TileOrder rationale).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "casr_common.h"
 #include "casr_internal.h"
 
@@ -176,6 +178,14 @@ constexpr int G16P_LDS = 2 * G16P_STAGE + 2 * G16_N;           // two stages + t
 constexpr int G16P_EPI_STORES = 32;                             // float4 stores per thread per tile
 static_assert(G16P_LDS * 4 <= 160 * 1024, "stages + bias slots fit the LDS");
 
+template <int I, int N, class F>
+CASR_DEV void static_for16(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for16<I + 1, N>(f);
+  }
+}
+
 template <int VM>
 CASR_DEV void g16_vm_wait() {
   static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
@@ -184,7 +194,11 @@ CASR_DEV void g16_vm_wait() {
 
 // DIAG (tools/probes/gemm16_probe.hip only; results then wrong for 1, 2, 4): 1 = no k-loop DMA
 // (stale LDS), 2 = no MFMA, 4 = no epilogue stores; 8 = iglp_opt(1) in the k loop, 16 = s_setprio 1
-// for waves 4-7 (both measured within noise)
+// for waves 4-7 (both measured within noise); 32 = the next stage's DMA issued two instructions
+// at a time between the first k-step's MFMA groups instead of in one burst after the barrier
+// (probe, bitwise equal: Kp 768 628-639 -> 599-618 us, Kp 512 445-467 -> 428-440 us; one per group
+// over both k-steps lands too late, 450-462 us; but inside the encoder, A/B in bench.py, the input
+// projections took 1.96-2.00 ms against 1.93: not launched)
 template <int DIAG = 0>
 __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __restrict__ A16,
                                                              const float* __restrict__ W16,
@@ -205,29 +219,38 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
     return L;
   };
   // DMA of stage (tile (n, m), k tile kt) into stage buffer `sb` (+ the tile's bias at kt = 0)
-  auto stage = [&](int sb, int n, int m, int kt, int tpar) {
+  // DMA slot q of a stage: rows i = q / 2 of this wave's share, A (q even) or W (q odd); the last
+  // slot also brings the tile's bias at kt = 0
+  constexpr int NQ = 2 * (RW / 8);
+  auto stage_slot = [&](int sb, int n, int m, int kt, int tpar, auto Q) {
+    constexpr int q = decltype(Q)::value, i = q >> 1;
     float* dst = lds + sb * G16P_STAGE;
     const int m0 = m * G16_M, n0 = n * G16_N, k0 = kt * G16_K;
-#pragma unroll
-    for (int i = 0; i < RW / 8; ++i) {
-      const int row = wave * RW + i * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
-      const int ar = min(m0 + row, M - 1), wr = min(n0 + row, N - 1);
-      float* la = dst + (wave * RW + i * 8) * G16_K;
-      lds_dma16(A16 + (size_t)ar * Kp + k0 + c * 4, la);
-      lds_dma16(W16 + (size_t)wr * Kp + k0 + c * 4, la + G16_TILE);
+    const int row = wave * RW + i * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+    float* la = dst + (wave * RW + i * 8) * G16_K;
+    if constexpr ((q & 1) == 0) {
+      lds_dma16(A16 + (size_t)min(m0 + row, M - 1) * Kp + k0 + c * 4, la);
+    } else {
+      lds_dma16(W16 + (size_t)min(n0 + row, N - 1) * Kp + k0 + c * 4, la + G16_TILE);
     }
-    if (kt == 0 && wave == 0) lds_dma16(bias + min(n0 + lane * 4, N - 4), bias_lds + tpar * G16_N);
+    if constexpr (q == NQ - 1) {
+      if (kt == 0 && wave == 0) lds_dma16(bias + min(n0 + lane * 4, N - 4), bias_lds + tpar * G16_N);
+    }
   };
+  auto stage = [&](int sb, int n, int m, int kt, int tpar) {
+    static_for16<0, NQ>([&](auto Q) { stage_slot(sb, n, m, kt, tpar, Q); });
+  };
+  constexpr bool IL = (DIAG & 32) != 0;
 
   f32x16 acc[4][NT];
   const _Float16 two11 = (_Float16)2048.0f;
   if ((DIAG & 16) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  auto compute = [&](const float* src) {
+  auto compute = [&](const float* src, auto&& issue) {
     const float* as = src;
     const float* ws = src + G16_TILE;
     if constexpr ((DIAG & 8) != 0) __builtin_amdgcn_iglp_opt(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    static_for16<0, 2>([&](auto KS) {
+      constexpr int ks = decltype(KS)::value;
       const int ch = 2 * ks + hsel;
       f16x8 wh[NT], wl[NT], w1[NT];
 #pragma unroll
@@ -237,8 +260,8 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
         wl[t] = *reinterpret_cast<const f16x8*>(ws + row * G16_K + (((4 + ch) ^ sw) << 2));
         w1[t] = wh[t] * two11;
       }
-#pragma unroll
-      for (int tm = 0; tm < 4; ++tm) {
+      static_for16<0, 4>([&](auto TM) {
+        constexpr int tm = decltype(TM)::value;
         const int row = wm * 128 + tm * 32 + r32, sw = (row >> 1) & 7;
         const f16x8 ah = *reinterpret_cast<const f16x8*>(as + row * G16_K + ((ch ^ sw) << 2));
         const f16x8 al = *reinterpret_cast<const f16x8*>(as + row * G16_K + (((4 + ch) ^ sw) << 2));
@@ -248,8 +271,12 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
           acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl[t], acc[tm][t], 0, 0, 0);
           acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh[t], acc[tm][t], 0, 0, 0);
         }
-      }
-    }
+        if constexpr (IL && ks == 0) {  // NQ = 8 slots over the 4 groups of the first k-step
+          issue(std::integral_constant<int, 2 * tm>{});
+          issue(std::integral_constant<int, 2 * tm + 1>{});
+        }
+      });
+    });
   };
   auto barrier = [] {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -279,11 +306,14 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
       else g16_vm_wait<0>();
       after_epi = 0;
       barrier();  // everyone's DMA of this stage landed; everyone is done reading the other buffer
-      if (!(DIAG & 1)) {
-        if (kt + 1 < nk) stage(sb ^ 1, n, m, kt + 1, tpar);
-        else if (L2 < total) stage(sb ^ 1, n2, m2, 0, tpar ^ 1);
-      }
-      if (!(DIAG & 2)) compute(lds + sb * G16P_STAGE);
+      auto issue = [&](auto Q) {
+        if (DIAG & 1) return;
+        if (kt + 1 < nk) stage_slot(sb ^ 1, n, m, kt + 1, tpar, Q);
+        else if (L2 < total) stage_slot(sb ^ 1, n2, m2, 0, tpar ^ 1, Q);
+      };
+      if constexpr (!IL) static_for16<0, NQ>(issue);
+      if (!(DIAG & 2)) compute(lds + sb * G16P_STAGE, issue);
+      else if constexpr (IL) static_for16<0, NQ>(issue);
       sb ^= 1;
     }
     // epilogue through the stage buffer just consumed (sb ^ 1 now): four rounds of two 32-row
@@ -372,8 +402,8 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
       return v > 0 ? v : 256;
     }();
     const int total = order.blocks();
-    hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, M, N,
-                       Kp, order, total);
+    hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
+                       M, N, Kp, order, total);
   } else if (gemm16_waves() == 8)
     hipLaunchKernelGGL(gemm16_bias_kernel<4>, dim3(order.blocks()), dim3(512), 0, s, X16, W16, bias, Gin, M, N, Kp,
                        order);
