@@ -163,6 +163,7 @@ struct casr_handle {
   // encoder workspace
   DevBuf gin, out0, out1, hbuf, cst, hfin, keysT, lens;
   DevBuf feat;     // casr_encode_fbank outside the s16x3 image path: the f32 features
+  DevBuf fstat;    // feature statistics scratch [B][2][D] (features.hip)
   DevBuf hx;       // persistent recurrence: tagged h words [3][2][Bp][H]
   DevBuf eflag;    // encoder device guard bits (CASR_DEV_REC_TIMEOUT)
   DevBuf fe_const; // FrontendConst (filterbank, window, twiddles), built on first casr_log_mel
@@ -453,7 +454,7 @@ void casr_destroy(casr_handle* h) {
     if (h->ev_out[i]) (void)hipEventDestroy(h->ev_out[i]);
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
-  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->hx, &h->x16, &h->eflag, &h->fe_const, &h->fflag,
+  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->eflag, &h->fe_const, &h->fflag,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout})
     b->release();
   delete h;
@@ -484,7 +485,8 @@ int casr_features(casr_handle* h, const float* fbank, const int32_t* frames, int
     return fail(h, CASR_ERR_ARG, "casr_features: bad arguments (B=%d T=%d)", B, T);
   HIP_OK(h, hipSetDevice(h->device));
   ProfScope ps(&h->prof, CASR_K_FEATURES, (hipStream_t)stream);
-  HIP_OK(h, launch_features(fbank, frames, B, T, eps, feat, feat_len, (hipStream_t)stream));
+  HIP_OK(h, h->fstat.ensure((size_t)B * 2 * D * sizeof(float)));
+  HIP_OK(h, launch_features(fbank, frames, B, T, eps, feat, feat_len, h->fstat.as<float>(), (hipStream_t)stream));
   return CASR_OK;
 }
 
@@ -562,13 +564,15 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
   bool x16_ready = false;
   if (fb) {
     ProfScope ps(&h->prof, CASR_K_FEATURES, s);
+    HIP_OK(h, h->fstat.ensure((size_t)B * 2 * D * sizeof(float)));
     if (s16 && features_x16_supported(T)) {
-      HIP_OK(h, launch_features_x16(fb, frames, B, T, eps, h->lens.as<int32_t>(), h->x16.as<uint16_t>(), s16_kpad(D),
+      HIP_OK(h, launch_features_x16(fb, frames, B, T, eps, h->lens.as<int32_t>(), h->fstat.as<float>(),
+                                    h->x16.as<uint16_t>(), s16_kpad(D),
                                     h->eflag.as<int32_t>(), s));
       x16_ready = true;  // feat stays NULL: layer 0 reads only the image (no residual input)
     } else {
       HIP_OK(h, h->feat.ensure(rows * D * sizeof(float)));
-      HIP_OK(h, launch_features(fb, frames, B, T, eps, h->feat.as<float>(), h->lens.as<int32_t>(), s));
+      HIP_OK(h, launch_features(fb, frames, B, T, eps, h->feat.as<float>(), h->lens.as<int32_t>(), h->fstat.as<float>(), s));
       feat = h->feat.as<float>();
     }
   }

@@ -169,10 +169,11 @@ hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nma
 // features.hip
 // the layer-0 s16 row image straight from fbank (features_fused_kernel<true>, T / 3 <= 272)
 bool features_x16_supported(int T);
+// stats: [B][2][D] floats of scratch (per-utterance mean and std + eps of the 720 dimensions)
 hipError_t launch_features_x16(const float* fbank, const int32_t* frames, int B, int T, float eps,
-                               int32_t* feat_len, uint16_t* x16, int Kp, int32_t* err, hipStream_t s);
+                               int32_t* feat_len, float* stats, uint16_t* x16, int Kp, int32_t* err, hipStream_t s);
 hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int T, float eps,
-                           float* feat, int32_t* feat_len, hipStream_t s);
+                           float* feat, int32_t* feat_len, float* stats, hipStream_t s);
 hipError_t launch_gather_utts(const float* const* ptrs, const int32_t* lens, int B, int Tp,
                               float* feat, hipStream_t s);
 

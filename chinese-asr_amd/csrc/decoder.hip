@@ -114,6 +114,7 @@ template <int WR, int NT, int S, class ASrc, class Epi, bool S16 = false, int RS
 __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntiles, int nkt,
                                                     const float* __restrict__ Wf, ASrc asrc, Epi epi) {
   constexpr int KQ = 8 / (WR * WC), QPW = 4 / KQ, BM = 16 * WR * RS, NTW = NT / WC;
+  static_assert(128 % BM == 0, "row blocks tile the fused select's 128 token slots");
   static_assert(WR * WC * KQ == 8 && NT % WC == 0 && KQ <= 4, "8 waves = row groups x column groups x k slices");
   constexpr int ATILE = BM * DG_BK, WTILE = NT * FRAG;
   constexpr int STG = ATILE + WTILE;          // floats per stage: [A tile | W tile]
@@ -147,6 +148,9 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   const int r = lane & 15, g = lane >> 4;
   const int cnt_w = w < NDMA ? (NDMA - w + 7) / 8 : 0;  // DMA instructions this wave issues per stage
 
+  // the A source's own prologue (DecLstmA with a fused greedy select: the tokens of this block's
+  // rows, into LDS, before any row is bound); block-uniform, ends with a barrier when it runs
+  asrc.prologue(rb * BM, BM, nb == 0);
   // per-lane DMA sources that do not depend on k: A row segment bases, W fragment block bases
   int bad = 0;
   const float* aseg[NSLOT][2];
@@ -348,6 +352,28 @@ static void launch_dg(int NB, int R, int ntiles, int nkt, const float* Wf, const
 // A rows of the decoder LSTM: [embed(tok[r]) | st_old[src[r]][0:1024] = ctx | h]; a 64-deep
 // k tile lies in one segment (E = 256 is a multiple of 64).  Rows >= R read row R-1 (unused).
 // s16: emb is the split-word table (emb16) and the state segment starts at ST16 ([ctx16 | h16]).
+// Greedy select of step lsel fused into the next step's LSTMCell (run_greedy): the partials of
+// the projection (GreedyPart, one per 80-column block) are reduced by the LSTMCell blocks
+// themselves, each for its own rows, so no select launch (and no kernel boundary) sits between
+// the projection and the next LSTMCell.  Every column block of a row block computes its rows'
+// tokens (32 rows x 64 partials); the block with nb == 0 also does the bookkeeping of
+// greedy_select_part_kernel (tokens, finished, lengths, score, newdone), with the same
+// arithmetic, so both forms give the same bits.
+struct GreedySel {
+  GreedyPart gp;
+  int nbp, lsel, L, eos;
+  uint8_t* fin;
+  int32_t* out_len;
+  float* accum;
+  int32_t* tokens;
+  int32_t* newdone;
+};
+
+__device__ __forceinline__ int* sel_tok_lds() {
+  __shared__ int t[128];
+  return t;
+}
+
 struct DecLstmA {
   static constexpr int kSeg = E;  // k < kSeg: embedding row, else state row
   const float* emb;
@@ -356,11 +382,62 @@ struct DecLstmA {
   const int32_t* src;
   int32_t* err;
   int R, V, s16;
+  int sel = 0;  // 1: tokens from the fused greedy select of step gs.lsel (prologue)
+  GreedySel gs = {};
+  __device__ __forceinline__ void prologue(int row0, int bm, bool writer) const {
+    if (!sel) return;
+    int* st = sel_tok_lds();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool all_done = done_before(gs.newdone, gs.lsel) >= R;  // greedy_select_part_kernel's skip
+    for (int i = w; i < bm; i += 8) {
+      const int r = row0 + i;
+      if (r >= R) break;
+      if (all_done) {  // every row finished before step lsel: nothing downstream runs any more
+        if (lane == 0) st[r & 127] = 0;
+        continue;
+      }
+      float m = -INFINITY, se = 0.f;
+      int mi = 0x7fffffff;
+      if (lane < gs.nbp) {
+        m = gs.gp.mx[(size_t)r * GP_NB + lane];
+        se = gs.gp.se[(size_t)r * GP_NB + lane];
+        mi = gs.gp.ix[(size_t)r * GP_NB + lane];
+      }
+      float gm = m;
+      int gi = mi;
+      wave_best(gm, gi);
+      int t = gi;
+      const bool bad_t = (unsigned)t >= (unsigned)V;  // no finite maximum (NaN row)
+      if (bad_t) t = 0;
+      if (lane == 0) st[r & 127] = t;  // BM divides 128 and row0: distinct slots
+      if (!writer) continue;
+      const float sx = wave_sum((se > 0.f) ? se * expf(m - gm) : 0.f);
+      if (lane != 0) continue;
+      if (bad_t) atomicOr(err, CASR_DEV_NAN_LOGITS);
+      const float lp = gm - (logf(sx) + gm);
+      gs.tokens[(size_t)r * gs.L + gs.lsel] = t;
+      const bool was = gs.fin[r] != 0;
+      const bool cur = t == gs.eos;
+      float acc = gs.accum[r];
+      if (!was && cur) acc = acc + lp;  // model.py:567
+      const bool now = was || cur;
+      if (!now) {
+        gs.out_len[r] += 1;  // model.py:573
+        acc = acc + lp;      // model.py:576
+      }
+      gs.accum[r] = acc;
+      if (now && !was) {
+        gs.fin[r] = 1;
+        atomicAdd(&gs.newdone[gs.lsel], 1);
+      }
+    }
+    __syncthreads();
+  }
   // branch-free (a branch on a loaded index would serialise the prologue's loads: one round
   // trip each); bad indices are clamped and reported through `bad` (CASR_DEV_* bits)
   __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1, int& bad) const {
     row = row < R ? row : R - 1;
-    const int t = tok[row];
+    const int t = sel ? sel_tok_lds()[row & 127] : tok[row];
     const bool bt = (unsigned)t >= (unsigned)V;
     bad |= bt ? CASR_DEV_BAD_TOKEN : 0;
     seg0 = emb + (size_t)(bt ? 0 : t) * E;
@@ -452,6 +529,7 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
   static constexpr int kSeg = 0;
   const float* st;
   int R, s16;
+  __device__ __forceinline__ void prologue(int, int, bool) const {}
   __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1, int&) const {
     seg0 = seg1 = st + (size_t)(row < R ? row : R - 1) * ST + (s16 ? ST16 : 0);
   }
@@ -575,10 +653,11 @@ struct ProjEpi {
 // ------------------------------------------------------------------ init
 // st0[r] = [ctx 0 | h_fin(b) | c_fin(b)], tok = sos, src = r, score = 0 (model.py:531-535,
 // :660-669, :684-690).
+// src2 (greedy with the fused select, else null): the second predecessor buffer, also identity
 __global__ void decode_init_kernel(float* __restrict__ st0, const float* __restrict__ hfin,
                                    const float* __restrict__ cfin, int B, int k, int sos,
                                    int32_t* __restrict__ tok, int32_t* __restrict__ src,
-                                   float* __restrict__ score) {
+                                   float* __restrict__ score, int32_t* __restrict__ src2) {
   const int r = blockIdx.x, b = r / k;
   float* o = st0 + (size_t)r * ST;
   for (int i = threadIdx.x; i < ST16; i += blockDim.x) {
@@ -599,6 +678,7 @@ __global__ void decode_init_kernel(float* __restrict__ st0, const float* __restr
     tok[r] = sos;
     src[r] = r;
     score[r] = 0.f;
+    if (src2) src2[r] = r;
   }
 }
 
@@ -1408,13 +1488,17 @@ static bool row_partials(const DecodeArgs& a) {
 }
 
 static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
-                              hipStream_t s) {
+                              hipStream_t s, const GreedySel* gsel = nullptr) {
   const int R = a.B * a.k;
   const float* st_old = d.st[l & 1];
   float* st_new = d.st[(l + 1) & 1];
   {
     ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
     DecLstmA asrc{a.W + (a.s16 ? a.L.emb16 : a.L.emb), st_old, d.tok[l & 1], d.src[l & 1], d.err, R, a.V, a.s16};
+    if (gsel) {
+      asrc.sel = 1;
+      asrc.gs = *gsel;
+    }
     DecLstmEpi epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, a.W + a.L.w_hidden, d.qpart, R, l, total};
     launch_dec_lstm(R, a.W + (a.s16 ? a.L.dec_w16 : a.L.dec_w), asrc, epi, a.s16, s);
   }
@@ -1480,11 +1564,22 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
   if (e0 == hipSuccess) e0 = fill_u32(accum, 0, R, s);
   if (e0 == hipSuccess) e0 = fill_u32(tokens, 0xffffffffu, (size_t)R * a.max_len, s);
   if (e0 != hipSuccess) return e0;
+  // the select of step l runs inside step l+1's LSTMCell (GreedySel) when the projection writes
+  // per-block partials; the last step's select is a launch of its own.  CASR_FUSE_SELECT=0 keeps
+  // every select a launch (A/B knob, read at every call; the same bits either way)
+  const bool fuse_env = [] {
+    const char* e = std::getenv("CASR_FUSE_SELECT");
+    return !e || std::atoi(e) != 0;
+  }();
+  const bool fuse = fuse_env && row_partials(a);
   hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, 1,
-                     a.sos, d.tok[0], d.src[0], d.score[0]);
+                     a.sos, d.tok[0], d.src[0], d.score[0], fuse ? d.src[1] : nullptr);
   for (int l = 0; l < a.max_len; ++l) {
-    hipError_t e = decode_step(a, d, l, R, align ? align + (size_t)l * a.Tp * R : nullptr, s);
+    GreedySel gs{d.part, proj_col_blocks(a), l - 1, a.max_len, a.eos, finished, out_len, accum, tokens, d.newdone};
+    hipError_t e = decode_step(a, d, l, R, align ? align + (size_t)l * a.Tp * R : nullptr, s,
+                               fuse && l > 0 ? &gs : nullptr);
     if (e != hipSuccess) return e;
+    if (fuse && l + 1 < a.max_len) continue;
     ProfScope ps(a.prof, CASR_K_SELECT, s);
     if (row_partials(a)) {
       hipLaunchKernelGGL(greedy_select_part_kernel, dim3((R + 3) / 4), dim3(256), 0, s, d.part, proj_col_blocks(a), a.V,
@@ -1517,7 +1612,7 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
   if (e0 == hipSuccess) e0 = fill_u8(d.topfin, 0, a.B, s);
   if (e0 != hipSuccess) return e0;
   hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, a.k,
-                     a.sos, d.tok[0], d.src[0], d.score[0]);
+                     a.sos, d.tok[0], d.src[0], d.score[0], nullptr);
   for (int l = 0; l < a.max_len; ++l) {
     hipError_t e = decode_step(a, d, l, a.B, nullptr, s);
     if (e != hipSuccess) return e;

@@ -219,6 +219,41 @@ def test_graph_replay_equals_eager(eng):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("eos_bias", [0.0, 12.0])
+def test_fused_select_equals_select_launches(eng, eos_bias):
+    """Greedy decoding with each step's select fused into the next LSTMCell (default) and with
+    every select a launch of its own (CASR_FUSE_SELECT=0) give the same tokens, lengths, scores
+    and finished flags bit for bit: ragged lengths, B = 200 (a partial row block), without and
+    with early finishers (eos_bias: rows end at different steps, the early exit counts them)."""
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True, eos_bias=eos_bias)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    B = 200
+    rs = np.random.RandomState(5)
+    frames = rs.randint(30, 400, size=B)
+    x = np.zeros((B, 400, 80), np.float32)
+    for b in range(B):
+        x[b, :frames[b]] = fbank_for(b, int(frames[b]))
+    feat, flen = eng.features(torch.from_numpy(x).to(eng.device),
+                              torch.from_numpy(frames.astype(np.int32)).to(eng.device))
+    eng.encode(feat, flen)
+    outs = []
+    try:
+        eng.set_graphs(False)
+        for fuse in ("0", "1"):
+            os.environ["CASR_FUSE_SELECT"] = fuse
+            g = eng.greedy()
+            assert eng.device_flags() == 0
+            outs.append({k: v.cpu() for k, v in g.items() if torch.is_tensor(v)})
+    finally:
+        os.environ.pop("CASR_FUSE_SELECT", None)
+        eng.set_graphs(True)
+    assert outs[0].keys() == outs[1].keys() and "tokens" in outs[0]
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    if eos_bias:
+        assert bool(outs[1]["finished"].any()), "with the EOS bias some rows must finish early"
+
+
 @pytest.mark.parametrize("B", [37, 256])
 def test_persistent_recurrence_equals_per_step(eng, B):
     """The persistent per-layer recurrence (granule hand-offs, either store flavour) and the
