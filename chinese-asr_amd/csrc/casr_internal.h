@@ -167,7 +167,7 @@ hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nma
                           const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s);
 
 // features.hip
-// the layer-0 s16 row image straight from fbank (features_fused_kernel<true>, T / 3 <= 272)
+// the layer-0 s16 row image straight from fbank (features_rows_kernel<true>, T <= 1024)
 bool features_x16_supported(int T);
 // stats: [B][2][D] floats of scratch (per-utterance mean and std + eps of the 720 dimensions)
 hipError_t launch_features_x16(const float* fbank, const int32_t* frames, int B, int T, float eps,

@@ -121,12 +121,12 @@ __global__ __launch_bounds__(256) void cmvn_kernel(float* __restrict__ feat,
 
 // Two kernels for T <= FS_MAX_T (the common case; longer utterances take the two-pass kernels
 // above):
-//   features_stats_kernel: grid (F / SM mel slabs, B), block SQ x SPH threads = 144 output
-//     dimensions (3 channels x 3 stacked frames x SM = 16 mels) x 4 time chunks.  The block's
-//     fbank columns (nf x 16 floats) are staged in LDS once; each thread sweeps its chunk of output
-//     rows twice (sum, then centred second moment) with a 9-frame register window that slides by
-//     3 frames per row (3 LDS reads per value), and the statistics (mean, std + eps) of the
-//     utterance's 720 dimensions go to a [B][2][D] buffer.
+//   features_stats_kernel: grid (F / SM mel slabs, B), block 576 threads = 24 (stacked frame,
+//     mel) pairs (3 x SM = 8 mels) x 24 time chunks.  The block's fbank columns (nf x 8 floats) are
+//     staged in LDS once; each thread sweeps its chunk of output rows twice (sum, then centred
+//     second moment) with a 9-frame register window that slides by 3 frames per row, computing
+//     the three channels of its pair from the same window, and the statistics (mean, std + eps) of
+//     the utterance's 720 dimensions go to a [B][2][D] buffer.
 //   features_rows_kernel: grid (ceil(Tp / RJ), B), block 384 = one thread per column PAIR of an
 //     output row (768 columns: the 720 features and the zero pad of the s16 image), RJ rows per
 //     block from an LDS window of 3 RJ + 8 frames x 80 mels, so every row is written whole by one
@@ -136,36 +136,52 @@ __global__ __launch_bounds__(256) void cmvn_kernel(float* __restrict__ feat,
 // 68 registers: 152 VGPRs, one block per CU; stores of 32-B pieces) took 0.25 ms at B = 256, T =
 // 800 (0.14 of it compute, the rest stores).
 // Arithmetic: every feature value is fmaf over the 9 taps in tap order with zero frames outside
-// [0, nf) (stack_kernel's); mean = ((s0 + s1) + (s2 + s3)) / lp over the four chunk sums (each in
-// row order), var likewise over (v - mean)^2 / (lp - 1), std = sqrt(var) + eps (main.py:37).
-constexpr int SM = 16, SQ = 9 * SM, SPH = 4;
-constexpr int FS_MAX_T = 900;  // stats kernel's LDS: nf x SM floats (56 KB) + 3 KB, under 64 KB
+// [0, nf) (stack_kernel's); mean = the 24 chunk sums (each in row order) added in a fixed tree,
+// / lp; var likewise over (v - mean)^2 / (lp - 1); std = sqrt(var) + eps (main.py:37).
+constexpr int SM = 8, SRM = 3 * SM, SPH = 24, SQ = 9 * SM;  // mels, (frame, mel) pairs, chunks, dims
+constexpr int FS_MAX_T = 1024;  // stats kernel's LDS: nf x SM floats (32 KB) + 7 KB
 constexpr int RJ = 16, RNF = 3 * RJ + 8, RTH = 384;
 static_assert(F % SM == 0 && 2 * RTH >= D, "mel slabs tile the 80 mels; a block's pairs cover a row");
 
-__global__ __launch_bounds__(SQ * SPH) void features_stats_kernel(const float* __restrict__ fbank,
-                                                                  const int32_t* __restrict__ frames, int T,
-                                                                  float eps, float* __restrict__ stats,
-                                                                  int32_t* __restrict__ feat_len) {
+// one thread per (stacked frame r, mel) pair and time chunk: the three channels (identity, delta,
+// delta-delta) of a pair read the same 9-frame window, so they are computed together
+__global__ __launch_bounds__(SRM * SPH) void features_stats_kernel(const float* __restrict__ fbank,
+                                                                   const int32_t* __restrict__ frames, int B, int T,
+                                                                   float eps, float* __restrict__ stats,
+                                                                   int32_t* __restrict__ feat_len) {
   extern __shared__ float xs[];  // [nf][SM]
   __shared__ float part[SPH][SQ];
   __shared__ float mean_s[SQ];
-  const int m0 = blockIdx.x * SM, b = blockIdx.y;
-  const int tid = threadIdx.x, q = tid % SQ, ph = tid / SQ;
+  // 1-D grid, XCD-aware: the F / SM slab blocks of one utterance take ids with equal id % 8, so
+  // they run on one XCD and its L2 fetches each 320-B fbank row once for all of them (each block
+  // reads a 32-B piece of every row; spread over the XCDs every piece cost a line fetch of its own)
+  constexpr int NS = F / SM;
+  const int L = blockIdx.x, xq = L & 7, jq = L >> 3;
+  const int b = (jq / NS) * 8 + xq, m0 = (jq % NS) * SM;
+  if (b >= B) return;
+  const int tid = threadIdx.x, rm = tid % SRM, ph = tid / SRM;
   const int nf = min(max(frames[b], 0), T);
   const int lp = nf / 3;
-  if (blockIdx.x == 0 && tid == 0) feat_len[b] = lp;
+  if (m0 == 0 && tid == 0) feat_len[b] = lp;
   const float* x = fbank + (size_t)b * T * F + m0;
-  for (int i = tid; i < nf * (SM / 4); i += SQ * SPH) {
-    const int t = i / (SM / 4), c4 = i % (SM / 4);
-    *reinterpret_cast<float4*>(xs + t * SM + 4 * c4) = *reinterpret_cast<const float4*>(x + (size_t)t * F + 4 * c4);
+  // every staging load of a thread in flight before its first LDS store
+  constexpr int NLD = (FS_MAX_T * (SM / 4) + SRM * SPH - 1) / (SRM * SPH);
+  float4 ld[NLD];
+#pragma unroll
+  for (int u = 0; u < NLD; ++u) {
+    const int i = tid + u * SRM * SPH;
+    ld[u] = make_float4(0.f, 0.f, 0.f, 0.f);  // (left undefined, hipcc kept the array in scratch)
+    if (i < nf * (SM / 4)) ld[u] = *reinterpret_cast<const float4*>(x + (size_t)(i / (SM / 4)) * F + 4 * (i % (SM / 4)));
+  }
+#pragma unroll
+  for (int u = 0; u < NLD; ++u) {
+    const int i = tid + u * SRM * SPH;
+    if (i < nf * (SM / 4)) *reinterpret_cast<float4*>(xs + (i / (SM / 4)) * SM + 4 * (i % (SM / 4))) = ld[u];
   }
   __syncthreads();
-  // dimension q = (c * 3 + r) * SM + mm  ->  output column c*240 + r*80 + m0 + mm
-  const int cr = q / SM, mm = q % SM, c = cr / 3, r = cr % 3;
-  const int o = c * 3 * F + r * F + m0 + mm;
+  // pair rm = r * SM + mm; its dims q = c * SRM + rm  ->  output column c*240 + r*80 + m0 + mm
+  const int r = rm / SM, mm = rm % SM;
   const DeltaTaps taps = make_taps();
-  const float* w = (c == 1) ? taps.d1 : taps.d2;
   const int ch = (lp + SPH - 1) / SPH, ja = min(ph * ch, lp), jb = min(ja + ch, lp);
   auto frame = [&](int t) { return (t >= 0 && t < nf) ? xs[t * SM + mm] : 0.f; };
   auto sweep = [&](auto&& use) {
@@ -173,39 +189,63 @@ __global__ __launch_bounds__(SQ * SPH) void features_stats_kernel(const float* _
 #pragma unroll
     for (int k = 0; k < 9; ++k) win[k] = frame(3 * ja + r + k - 4);
     for (int j = ja; j < jb; ++j) {
-      float v = 0.f;
-      if (c == 0) {
-        v = win[4];
-      } else {
+      float v1 = 0.f, v2 = 0.f;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) v = fmaf(w[k], win[k], v);  // as oneDNN's conv2d (torch's tap order)
+      for (int k = 0; k < 9; ++k) {  // as oneDNN's conv2d (torch's tap order)
+        v1 = fmaf(taps.d1[k], win[k], v1);
+        v2 = fmaf(taps.d2[k], win[k], v2);
       }
-      use(v);
+      use(win[4], v1, v2);
 #pragma unroll
       for (int k = 0; k < 6; ++k) win[k] = win[k + 3];
 #pragma unroll
       for (int k = 6; k < 9; ++k) win[k] = frame(3 * (j + 1) + r + k - 4);
     }
   };
-  float s = 0.f;
-  sweep([&](float v) { s += v; });
-  part[ph][q] = s;
+  // fixed-order sum of the SPH = 24 chunk partials of dim q: three groups of eight
+  auto chunks = [&](int q) {
+    auto g8 = [&](int g) {
+      const float* p = &part[8 * g][q];
+      return ((p[0] + p[SQ]) + (p[2 * SQ] + p[3 * SQ])) + ((p[4 * SQ] + p[5 * SQ]) + (p[6 * SQ] + p[7 * SQ]));
+    };
+    return (g8(0) + g8(1)) + g8(2);
+  };
+  static_assert(SPH == 24, "chunks() sums 24 partials");
+#ifdef CASR_FEAT_DIAG  // diagnostic build: staging only
+  if (xs[tid] == 1234.5f) stats[0] = 1.f;
+  return;
+#endif
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+  sweep([&](float v0, float v1, float v2) {
+    s0 += v0;
+    s1 += v1;
+    s2 += v2;
+  });
+  part[ph][rm] = s0;
+  part[ph][SRM + rm] = s1;
+  part[ph][2 * SRM + rm] = s2;
   __syncthreads();
-  if (ph == 0) mean_s[q] = ((part[0][q] + part[1][q]) + (part[2][q] + part[3][q])) / (float)lp;
+  if (tid < SQ) mean_s[tid] = chunks(tid) / (float)lp;
   __syncthreads();
-  const float mean = mean_s[q];
-  float s2 = 0.f;
-  sweep([&](float v) {
-    const float dv = v - mean;
-    s2 += dv * dv;
+  const float mu0 = mean_s[rm], mu1 = mean_s[SRM + rm], mu2 = mean_s[2 * SRM + rm];
+  s0 = s1 = s2 = 0.f;
+  sweep([&](float v0, float v1, float v2) {
+    const float d0 = v0 - mu0, d1 = v1 - mu1, d2 = v2 - mu2;
+    s0 += d0 * d0;
+    s1 += d1 * d1;
+    s2 += d2 * d2;
   });
   __syncthreads();  // everyone has read part before it is reused
-  part[ph][q] = s2;
+  part[ph][rm] = s0;
+  part[ph][SRM + rm] = s1;
+  part[ph][2 * SRM + rm] = s2;
   __syncthreads();
-  if (ph == 0) {
-    const float var = ((part[0][q] + part[1][q]) + (part[2][q] + part[3][q])) / (float)(lp - 1);
+  if (tid < SQ) {
+    const int c = tid / SRM, rr = (tid % SRM) / SM, m = tid % SM;
+    const int o = c * 3 * F + rr * F + m0 + m;
+    const float var = chunks(tid) / (float)(lp - 1);
     float* st = stats + (size_t)b * 2 * D;
-    st[o] = mean;
+    st[o] = mean_s[tid];
     st[D + o] = sqrtf(var) + eps;
   }
 }
@@ -226,11 +266,18 @@ __global__ __launch_bounds__(RTH) void features_rows_kernel(const float* __restr
   const int nf = min(max(frames[b], 0), T), lp = nf / 3;
   const int t_lo = 3 * j0 - 4;
   const float* x = fbank + (size_t)b * T * F;
-  for (int i = p; i < RNF * (F / 4); i += RTH) {
-    const int fr = i / (F / 4), c4 = i % (F / 4), t = t_lo + fr;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (t >= 0 && t < nf) v = *reinterpret_cast<const float4*>(x + (size_t)t * F + 4 * c4);
-    *reinterpret_cast<float4*>(xs + fr * F + 4 * c4) = v;
+  constexpr int NLD = (RNF * (F / 4) + RTH - 1) / RTH;  // staging loads per thread, all in flight
+  float4 ld[NLD];
+#pragma unroll
+  for (int u = 0; u < NLD; ++u) {
+    const int i = p + u * RTH, fr = i / (F / 4), c4 = i % (F / 4), t = t_lo + fr;
+    ld[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < RNF * (F / 4) && t >= 0 && t < nf) ld[u] = *reinterpret_cast<const float4*>(x + (size_t)t * F + 4 * c4);
+  }
+#pragma unroll
+  for (int u = 0; u < NLD; ++u) {
+    const int i = p + u * RTH;
+    if (i < RNF * (F / 4)) *reinterpret_cast<float4*>(xs + (i / (F / 4)) * F + 4 * (i % (F / 4))) = ld[u];
   }
   __syncthreads();
   const int o0 = 2 * p;  // columns o0, o0 + 1: same channel and stacked frame, mels m, m + 1
@@ -296,7 +343,7 @@ hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int
   // eps < 0: no CMVN (the stacked features get_log_mel returns, data.py:226-249)
   if (T <= FS_MAX_T) {
     const size_t shm = (size_t)T * SM * sizeof(float);
-    hipLaunchKernelGGL(features_stats_kernel, dim3(F / SM, B), dim3(SQ * SPH), shm, s, fbank, frames, T, eps, stats,
+    hipLaunchKernelGGL(features_stats_kernel, dim3((F / SM) * ((B + 7) / 8 * 8)), dim3(SRM * SPH), shm, s, fbank, frames, B, T, eps, stats,
                        feat_len);
     hipLaunchKernelGGL(features_rows_kernel<false>, dim3((Tp + RJ - 1) / RJ, B), dim3(RTH), 0, s, fbank, frames, T, Tp,
                        eps >= 0.f ? stats : nullptr, feat, nullptr, 0, nullptr);
@@ -317,7 +364,7 @@ hipError_t launch_features_x16(const float* fbank, const int32_t* frames, int B,
   const int Tp = T / 3;
   if (B <= 0 || !features_x16_supported(T) || Kp != 2 * RTH) return hipErrorInvalidValue;
   const size_t shm = (size_t)T * SM * sizeof(float);
-  hipLaunchKernelGGL(features_stats_kernel, dim3(F / SM, B), dim3(SQ * SPH), shm, s, fbank, frames, T, eps, stats,
+  hipLaunchKernelGGL(features_stats_kernel, dim3((F / SM) * ((B + 7) / 8 * 8)), dim3(SRM * SPH), shm, s, fbank, frames, B, T, eps, stats,
                      feat_len);
   hipLaunchKernelGGL(features_rows_kernel<true>, dim3((Tp + RJ - 1) / RJ, B), dim3(RTH), 0, s, fbank, frames, T, Tp,
                      eps >= 0.f ? stats : nullptr, nullptr, reinterpret_cast<uint32_t*>(x16), Kp, err);

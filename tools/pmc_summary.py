@@ -24,7 +24,7 @@ CLASS_OF = {  # bench.py kernel classes -> kernel-name prefixes (after short())
     "proj": "dgemm_kernel<4, 5, 4, ProjA",
     "attention": "attention_kernel<1>",
     "select": "greedy_select_part_kernel",
-    "features": "features_fused_kernel",
+    "features": "features_rows_kernel<true>",
 }
 
 
