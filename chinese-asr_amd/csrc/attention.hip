@@ -51,6 +51,18 @@ CASR_DEV float tanh_fast(float x) {
   return __builtin_fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + e), 1.f);
 }
 
+// Two at a time: the multiply, the add and the fma as packed f32 (v_pk_mul / v_pk_add /
+// v_pk_fma_f32: two lanes' worth per instruction, each element rounded exactly as the scalar
+// form), the exp and rcp per element.  Bitwise equal to tanh_fast on each element; the score
+// phase is bound by this VALU work (with 4 beam rows per block, 136 K tanh per block and step).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+CASR_DEV f32x2 tanh_fast2(f32x2 x) {
+  const f32x2 y = x * (f32x2){2.8853900817779268f, 2.8853900817779268f};
+  const f32x2 d = (f32x2){1.f, 1.f} + (f32x2){__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)};
+  const f32x2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  return __builtin_elementwise_fma((f32x2){-2.f, -2.f}, r, (f32x2){1.f, 1.f});
+}
+
 // Memory-level parallelism is the design driver: one block (8 waves) per utterance and step
 // streams its keys (A x Tq f32) and values (len x C f32) once per step, so every phase keeps all
 // of a lane's loads of that phase in flight at once (one round trip per phase, not one per
@@ -134,10 +146,12 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 #pragma unroll
         for (int j = 0; j < KPB; ++j) {
           const float qa = qs[(ab + i) * KPB + j];
-          e4[j][0] = fmaf(tanh_fast(kv[i].x + qa), va, e4[j][0]);
-          e4[j][1] = fmaf(tanh_fast(kv[i].y + qa), va, e4[j][1]);
-          e4[j][2] = fmaf(tanh_fast(kv[i].z + qa), va, e4[j][2]);
-          e4[j][3] = fmaf(tanh_fast(kv[i].w + qa), va, e4[j][3]);
+          const f32x2 q2 = {qa, qa}, v2 = {va, va};
+          const f32x2 lo = tanh_fast2((f32x2){kv[i].x, kv[i].y} + q2);
+          const f32x2 hi = tanh_fast2((f32x2){kv[i].z, kv[i].w} + q2);
+          const f32x2 a01 = __builtin_elementwise_fma(lo, v2, (f32x2){e4[j][0], e4[j][1]});
+          const f32x2 a23 = __builtin_elementwise_fma(hi, v2, (f32x2){e4[j][2], e4[j][3]});
+          e4[j][0] = a01.x, e4[j][1] = a01.y, e4[j][2] = a23.x, e4[j][3] = a23.y;
         }
       }
     };
