@@ -191,7 +191,8 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
 
   float c = 0.f;
   // epilogue operands that do not depend on h (Gin gates, residual input) are software-pipelined
-  // one step ahead: step s+1's are issued right after step s's granule sweep, so they land
+  // one step ahead: step s+1's are issued after step s's MFMAs (round 2; right after the sweep
+  // before: rec 2.82-2.88 -> 2.62-2.63 ms per greedy batch), so they land
   // during the MFMAs / cell instead of in front of the next sweep's vmcnt(0) wait
   auto load_operands = [&](int s, float (&g)[4], float& xr) {
     if (s < len) {
@@ -309,7 +310,6 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       }
       if (tr && lane == 0) tr[s * 5 + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
-    load_operands(s + 1, gin_n, x_n);
     if constexpr (!FIRST) {
       if constexpr (S16) {
         f32x4 accx[4];
@@ -346,6 +346,10 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     f32x4 (*rb)[4][64] = red[s & 1];
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn) rb[w][tn][lane] = acc[tn];
+    // step s+1's operands: issued here, after this wave's MFMAs (the wave whose sweep completes
+    // last sets the step's pace, and its MFMAs no longer queue behind these loads), still ahead of
+    // the next sweep, whose vmcnt wait retires them before the cell uses them
+    load_operands(s + 1, gin_n, x_n);
     __syncthreads();
     // the 16 k-chunk partials of this cell and the quit flag in one round of LDS reads (the quit
     // test used to go first: one more LDS round trip on the step chain)

@@ -44,10 +44,19 @@ def main(B=256, T=800, path="/tmp/rec_trace.bin"):
     st = t[:, :, :, 3].max(axis=1).reshape(ngrp, npg, Tp)          # WG's last store per step
     done = t[:, :, :, 1].reshape(ngrp, npg, nw, Tp)
     lat = done[:, :, :, 1:] - st.max(axis=1)[:, None, None, :-1]
+    # critical-path pieces: per workgroup and step, the last wave's sweep -> the barrier (MFMA of
+    # that wave + partial exchange), the spread of the waves' sweep completions, and per group the
+    # spread of its producers' stores
+    crit = t[:, :, 1:, 2].min(axis=1) - t[:, :, 1:, 1].max(axis=1)
+    spread = t[:, :, 1:, 1].max(axis=1) - t[:, :, 1:, 1].min(axis=1)
+    gskew = st.max(axis=1) - st.min(axis=1)
     total = t[:, :, -1, 3].max() - t[:, :, 0, 0].min()
     print(f"grid {nwg} WGs x {nw} waves, Tp={Tp}; layer wall {total:.1f} us = {total / Tp:.2f} us/step")
     for name, a in (("sweep", sweep), ("mfma+barrier", mfma), ("cell+store", cell), ("period", period),
-                    ("handoff (last producer store -> sweep done)", lat)):
+                    ("handoff (last producer store -> sweep done)", lat),
+                    ("last wave's sweep -> barrier done (per WG)", crit),
+                    ("sweep completion spread over a WG's waves", spread),
+                    ("store spread over a group's producers", gskew[:, 1:])):
         q = np.percentile(a, [10, 50, 90])
         print(f"  {name:44s} p10 {q[0]:6.2f}  p50 {q[1]:6.2f}  p90 {q[2]:6.2f} us")
     print(f"  sweep passes p50 {np.median(passes):.0f}  p90 {np.percentile(passes, 90):.0f}  max {passes.max()}")
