@@ -123,7 +123,11 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   }
   const int ub = mem, rg = grp % nrg, d = grp / nrg;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int kc = w & 3, half = (w >> 2) % (RG / 16), uh = (w >> 2) / (RG / 16);
+  // waves w and w + 4 share a SIMD (a workgroup's waves are dealt to the 4 SIMDs cyclically): give
+  // them different k-chunks, so their sweeps wait for different producers and their MFMA bursts
+  // do not meet on one pipe (with kc = w & 3 both completed together, behind the same producers).
+  // Measured: rec 2.62-2.72 -> 2.59-2.63 ms per greedy batch (three interleaved rounds), beam equal
+  const int kc = (w + (w >> 2)) & 3, half = (w >> 2) % (RG / 16), uh = (w >> 2) / (RG / 16);
   const size_t plane = (size_t)Bp * H;  // granules per direction per buffer
 
   // ---- epilogue cell of this thread: batch row rl (of RG), unit u (of UW)
@@ -359,7 +363,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
 #pragma unroll
     for (int tn = 0; tn < 4; ++tn)
 #pragma unroll
-      for (int ww = 0; ww < 4; ++ww) part[tn][ww] = rb[hw + ww][tn][src_lane][reg];
+      for (int ww = 0; ww < 4; ++ww) part[tn][ww] = rb[hw + ((ww - (hw >> 2)) & 3)][tn][src_lane][reg];  // k-chunk ww
     const int quit = s_quit[s & 1];  // acted on below, before the first store of the step
     if (tr && lane == 0) tr[s * 5 + 2] = (uint32_t)__builtin_amdgcn_s_memrealtime();
 
