@@ -150,7 +150,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
 
   // the A source's own prologue (DecLstmA with a fused greedy select: the tokens of this block's
   // rows, into LDS, before any row is bound); block-uniform, ends with a barrier when it runs
-  asrc.prologue(rb * BM, BM, nb == 0);
+  asrc.template prologue<BM>(rb * BM, nb == 0);
   // per-lane DMA sources that do not depend on k: A row segment bases, W fragment block bases
   int bad = 0;
   const float* aseg[NSLOT][2];
@@ -384,46 +384,63 @@ struct DecLstmA {
   int R, V, s16;
   int sel = 0;  // 1: tokens from the fused greedy select of step gs.lsel (prologue)
   GreedySel gs = {};
-  __device__ __forceinline__ void prologue(int row0, int bm, bool writer) const {
+  // every load of the wave's BM / 8 rows (partials, and for the writer the bookkeeping state) is
+  // issued before the first reduction: one round trip for the block, not one per row
+  template <int BM>
+  __device__ __forceinline__ void prologue(int row0, bool writer) const {
     if (!sel) return;
+    constexpr int RPW = BM / 8;  // rows per wave
     int* st = sel_tok_lds();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float m[RPW], se[RPW], acc0[RPW];
+    int mi[RPW], len0[RPW];
+    uint8_t fin0[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = row0 + w + 8 * i;
+      m[i] = -INFINITY, se[i] = 0.f, mi[i] = 0x7fffffff;
+      acc0[i] = 0.f, len0[i] = 0, fin0[i] = 0;
+      if (r < R && lane < gs.nbp) {
+        m[i] = gs.gp.mx[(size_t)r * GP_NB + lane];
+        se[i] = gs.gp.se[(size_t)r * GP_NB + lane];
+        mi[i] = gs.gp.ix[(size_t)r * GP_NB + lane];
+      }
+      if (writer && r < R && lane == 0) {
+        fin0[i] = gs.fin[r];
+        acc0[i] = gs.accum[r];
+        len0[i] = gs.out_len[r];
+      }
+    }
     const bool all_done = done_before(gs.newdone, gs.lsel) >= R;  // greedy_select_part_kernel's skip
-    for (int i = w; i < bm; i += 8) {
-      const int r = row0 + i;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = row0 + w + 8 * i;
       if (r >= R) break;
       if (all_done) {  // every row finished before step lsel: nothing downstream runs any more
         if (lane == 0) st[r & 127] = 0;
         continue;
       }
-      float m = -INFINITY, se = 0.f;
-      int mi = 0x7fffffff;
-      if (lane < gs.nbp) {
-        m = gs.gp.mx[(size_t)r * GP_NB + lane];
-        se = gs.gp.se[(size_t)r * GP_NB + lane];
-        mi = gs.gp.ix[(size_t)r * GP_NB + lane];
-      }
-      float gm = m;
-      int gi = mi;
+      float gm = m[i];
+      int gi = mi[i];
       wave_best(gm, gi);
       int t = gi;
       const bool bad_t = (unsigned)t >= (unsigned)V;  // no finite maximum (NaN row)
       if (bad_t) t = 0;
       if (lane == 0) st[r & 127] = t;  // BM divides 128 and row0: distinct slots
       if (!writer) continue;
-      const float sx = wave_sum((se > 0.f) ? se * expf(m - gm) : 0.f);
+      const float sx = wave_sum((se[i] > 0.f) ? se[i] * expf(m[i] - gm) : 0.f);
       if (lane != 0) continue;
       if (bad_t) atomicOr(err, CASR_DEV_NAN_LOGITS);
       const float lp = gm - (logf(sx) + gm);
       gs.tokens[(size_t)r * gs.L + gs.lsel] = t;
-      const bool was = gs.fin[r] != 0;
+      const bool was = fin0[i] != 0;
       const bool cur = t == gs.eos;
-      float acc = gs.accum[r];
+      float acc = acc0[i];
       if (!was && cur) acc = acc + lp;  // model.py:567
       const bool now = was || cur;
       if (!now) {
-        gs.out_len[r] += 1;  // model.py:573
-        acc = acc + lp;      // model.py:576
+        gs.out_len[r] = len0[i] + 1;  // model.py:573
+        acc = acc + lp;               // model.py:576
       }
       gs.accum[r] = acc;
       if (now && !was) {
@@ -529,7 +546,8 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
   static constexpr int kSeg = 0;
   const float* st;
   int R, s16;
-  __device__ __forceinline__ void prologue(int, int, bool) const {}
+  template <int BM>
+  __device__ __forceinline__ void prologue(int, bool) const {}
   __device__ __forceinline__ void bind(int row, const float*& seg0, const float*& seg1, int&) const {
     seg0 = seg1 = st + (size_t)(row < R ? row : R - 1) * ST + (s16 ? ST16 : 0);
   }
