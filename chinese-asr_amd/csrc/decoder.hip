@@ -478,6 +478,7 @@ struct DecLstmEpi {
   const float* w_hidden;  // [HD][A]
   float* qpart;           // [HD/16][R][A]
   int R, l, total;
+  int hw = 0;  // s16x3 arithmetic: the hardware-exp cell (casr_common.h lstm_cell_hw, as the encoder's)
   // operands loaded before the k loop: gate biases, predecessor rows, this lane's W_hidden
   // fragments of the query partial (A/16 x 4 MFMA steps); c of the predecessor after it
   struct Pre {
@@ -517,8 +518,12 @@ struct DecLstmEpi {
       const int row = row0 + e;
       float h2 = 0.f, c2;
       if (row < R) {
-        lstm_cell(acc[0][e] + p.bg[0], acc[1][e] + p.bg[1], acc[2][e] + p.bg[2], acc[3][e] + p.bg[3], p.cold[e], h2,
-                  c2);
+        if (hw)  // performance arithmetic (~1e-7 absolute, like the encoder's s16x3 cell)
+          lstm_cell_hw(acc[0][e] + p.bg[0], acc[1][e] + p.bg[1], acc[2][e] + p.bg[2], acc[3][e] + p.bg[3], p.cold[e],
+                       h2, c2);
+        else  // f32 arithmetic: libm cell, torch's CPU formulas
+          lstm_cell(acc[0][e] + p.bg[0], acc[1][e] + p.bg[1], acc[2][e] + p.bg[2], acc[3][e] + p.bg[3], p.cold[e], h2,
+                    c2);
         st_new[(size_t)row * ST + C + U] = h2;
         st_new[(size_t)row * ST + C + HD + U] = c2;
         reinterpret_cast<uint32_t*>(st_new)[(size_t)row * ST + ST16 + C + U] = split16_word(h2);
@@ -1518,6 +1523,7 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
       asrc.gs = *gsel;
     }
     DecLstmEpi epi{a.W + a.L.dec_b, st_old, st_new, asrc, d.newdone, a.W + a.L.w_hidden, d.qpart, R, l, total};
+    epi.hw = a.s16;
     launch_dec_lstm(R, a.W + (a.s16 ? a.L.dec_w16 : a.L.dec_w), asrc, epi, a.s16, s);
   }
   hipError_t e;
