@@ -595,7 +595,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
                                         h->W + h->L.enc_bias[l], h->gin.as<float>(), s));
       else
         HIP_OK(h, launch_input_proj_s16_big(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
-                                            h->W + h->L.enc_bias[l], h->gin.as<float>(), s));
+                                            h->W + h->L.enc_bias[l], h->gin.as<float>(), s, din));
     } else {
       HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
                                   h->gin.as<float>(), s));

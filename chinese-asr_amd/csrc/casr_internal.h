@@ -186,8 +186,9 @@ hipError_t launch_input_proj_s16(const float* X16, int M, int Kp, const float* W
 // gemm16.hip: the same product on 256 x 256 tiles (Kp % 64 == 0); gemm16_waves() = 0 selects
 // the 128 x 128 kernel instead
 int gemm16_waves();
+// K: the real input width (the images are zero from K to Kp); 0 = Kp
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                     float* Gin, hipStream_t s);
+                                     float* Gin, hipStream_t s, int K = 0);
 hipError_t launch_split_rows(const float* X, int ldx, int M, int K, int Kp, uint16_t* out, int32_t* err,
                              hipStream_t s);
 inline int s16_kpad(int K) { return (K + 63) / 64 * 64; }  // even number of 32-k tiles (gemm16.hip)

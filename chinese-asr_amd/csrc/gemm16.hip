@@ -204,13 +204,13 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
                                                              const float* __restrict__ W16,
                                                              const float* __restrict__ bias,
                                                              float* __restrict__ Cout, int M, int N, int Kp,
-                                                             Order16 order, int total) {
+                                                             Order16 order, int total, int nk) {
   __shared__ __attribute__((aligned(16))) float lds[G16P_LDS];
   constexpr int WN = 4, NT = 2, RW = 32;  // 8 waves = 2 (M) x 4 (N) of 128 x 64; 32 staged rows per wave
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int r32 = lane & 31, hsel = lane >> 5;
-  const int G = gridDim.x, nk = Kp / G16_K;
+  const int G = gridDim.x;  // nk: 32-k stages to run (of the Kp / 32 in a row image)
   float* const bias_lds = lds + 2 * G16P_STAGE;
 
   // tiles of this workgroup: L = blockIdx.x + i G, skipping the order's empty slots
@@ -386,7 +386,7 @@ int gemm16_waves() {
 }
 
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                     float* Gin, hipStream_t s) {
+                                     float* Gin, hipStream_t s, int K) {
   const int N = 8 * H;
   if (Kp % (2 * G16_K) != 0 || M <= 0 || N % G16_N != 0) return hipErrorInvalidValue;
   const int NB = N / G16_N, NM = (M + G16_M - 1) / G16_M;
@@ -402,8 +402,11 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
       return v > 0 ? v : 256;
     }();
     const int total = order.blocks();
+    // the persistent kernel runs ceil(K / 32) stages of the Kp-wide images (both zero past K): layer
+    // 0 (K = 720, Kp = 768) skips the all-zero last stage
+    const int nk = (K > 0 && K <= Kp ? K + G16_K - 1 : Kp) / G16_K;
     hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
-                       M, N, Kp, order, total);
+                       M, N, Kp, order, total, nk);
   } else if (gemm16_waves() == 8)
     hipLaunchKernelGGL(gemm16_bias_kernel<4>, dim3(order.blocks()), dim3(512), 0, s, X16, W16, bias, Gin, M, N, Kp,
                        order);

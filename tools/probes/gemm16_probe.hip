@@ -86,25 +86,25 @@ int main() {
                                N, Kp, order);
           else if (v == 1)
             hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks());
+                               order, order.blocks(), Kp / G16_K);
           else if (v == 2)
             hipLaunchKernelGGL(gemm16_persist_kernel<1>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks());
+                               order, order.blocks(), Kp / G16_K);
           else if (v == 3)
             hipLaunchKernelGGL(gemm16_persist_kernel<8>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks());
+                               order, order.blocks(), Kp / G16_K);
           else if (v == 4)
             hipLaunchKernelGGL(gemm16_persist_kernel<16>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks());
+                               order, order.blocks(), Kp / G16_K);
           else if (v == 5)
             hipLaunchKernelGGL(gemm16_persist_kernel<24>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks());
+                               order, order.blocks(), Kp / G16_K);
           else if (v == 6)
             hipLaunchKernelGGL(gemm16_persist_kernel<32>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks());
+                               order, order.blocks(), Kp / G16_K);
           else
             hipLaunchKernelGGL(gemm16_persist_kernel<33>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks());
+                               order, order.blocks(), Kp / G16_K);
         }
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
@@ -116,10 +116,10 @@ int main() {
     // the bitwise check needs the persist result: rerun it last (CHECK_IL=1: the interleaved one)
     if (getenv("CHECK_IL"))
       hipLaunchKernelGGL(gemm16_persist_kernel<32>, dim3(256), dim3(512), 0, 0, dA, dW, dB, dC1, M, N, Kp,
-                         Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}, Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}.blocks());
+                         Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}, Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}.blocks(), Kp / G16_K);
     else
     hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(256), dim3(512), 0, 0, dA, dW, dB, dC1, M, N, Kp,
-                       Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}, Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}.blocks());
+                       Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}, Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}.blocks(), Kp / G16_K);
     CK(hipDeviceSynchronize());
     std::vector<float> c0((size_t)M * N), c1((size_t)M * N);
     CK(hipMemcpy(c0.data(), dC0, c0.size() * 4, hipMemcpyDeviceToHost));
