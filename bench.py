@@ -12,6 +12,7 @@ independent (no collective in the timed region except the start/stop barriers).
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -289,25 +290,60 @@ def main():
         lm = _StubLM()
         info = {}
 
-        def step_lm():
+        # Serving loop: batch i's device work (features, encoder, beam, records) is enqueued and
+        # its records copied into one of two pinned host buffers; the host then rescores batch
+        # i-1 while the GPU runs batch i.  Every batch is fully processed inside the timed
+        # region (the last one is drained before the clock stops).
+        pinned = [None, None]
+
+        def enqueue(slot):
             eng5.encode_fbank(fbl, frl)
             r = eng5.beam(kl, 1.5, 1.5)
-            toks, blen = r["tokens"].cpu().numpy(), r["length"].cpu().numpy()
-            rt, rs, rv = (x.cpu().numpy() for x in eng5.beam_records())
+            dev_out = (r["tokens"], r["length"], r["steps"]) + tuple(eng5.beam_records())
+            if pinned[slot] is None:
+                pinned[slot] = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in dev_out]
+            for h, x in zip(pinned[slot], dev_out):
+                h.copy_(x, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            return slot, ev
+
+        def finish(pend):
+            slot, ev = pend
+            ev.synchronize()
+            # one sequential copy out of the pinned (possibly uncached) buffers, then the gathers
+            toks, blen, steps, rt, rs, rv = (h.numpy().copy() for h in pinned[slot])
             recs = records_by_utterance(rt, rs, rv)
             best = {b: (toks[b, :blen[b]].tolist(), 0.0) for b in range(Bl)}
             best.update(second_pass_select(recs, i2w, lm, 1.5, 1.5))
-            info["steps"] = int(r["steps"].item())
+            info["steps"] = int(steps[0])
             info["rescored"] = sum(1 for v in recs.values() if len(v) > 1)
             return best
 
-        step_lm()
-        dtl = timed(step_lm, args.beam_steps)
+        def run_lm(n):
+            prev = None
+            for i in range(n):
+                cur = enqueue(i % 2)
+                if prev is not None:
+                    finish(prev)
+                prev = cur
+            return finish(prev)
+
+        run_lm(2)
+        # a serving process freezes its start-up heap: the host rescoring allocates ~10^5 small
+        # objects per batch, and each full cyclic-GC pass over the torch / numpy heap otherwise
+        # adds ~50 ms to the batch it lands in (measured, tools/probes/config5_probe.py)
+        gc.collect()
+        gc.freeze()
+        dtl = timed(lambda: run_lm(args.beam_steps), 1)
+        gc.unfreeze()
         lm_line = {"config": "BASELINE config 5: beam 16 + second-pass LM rescoring (stub LM, host)",
                    "k": kl, "batch_per_gpu": Bl, "value": Bl * world * args.beam_steps / dtl, "unit": "utt/s",
                    "ms_per_step": 1000.0 * dtl / args.beam_steps, "decode_steps": info.get("steps"),
                    "utterances_rescored": info.get("rescored"),
-                   "weights": "synthetic recipe with the EOS bias (hypotheses finish before step 40)"}
+                   "weights": "synthetic recipe with the EOS bias (hypotheses finish before step 40)",
+                   "pipelined": "host rescoring of batch i-1 overlaps the device work of batch i "
+                                "(records double-buffered in pinned host memory)"}
         eng5.close()
 
     # side measurement: the same greedy step on the exact-f32 MFMA path (not the headline)

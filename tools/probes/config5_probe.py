@@ -44,6 +44,48 @@ def main():
         print(f"iter {it}: device {1e3 * (t[1] - t[0]):.2f} ms, records copy {1e3 * (t[2] - t[1]):.2f} ms, "
               f"assembly {1e3 * (t[3] - t[2]):.2f} ms, rescoring {1e3 * (t[4] - t[3]):.2f} ms; "
               f"{n} records, steps {int(r['steps'].item())}", flush=True)
+    # the bench's pipelined loop (bench.py config 5), per batch: enqueue, wait, host times
+    pinned = [None, None]
+
+    def enqueue(slot):
+        t0 = time.perf_counter()
+        eng.encode_fbank(fb, fr)
+        r = eng.beam(k, 1.5, 1.5)
+        dev_out = (r["tokens"], r["length"], r["steps"]) + tuple(eng.beam_records())
+        if pinned[slot] is None:
+            pinned[slot] = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in dev_out]
+        for h, x in zip(pinned[slot], dev_out):
+            h.copy_(x, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return slot, ev, time.perf_counter() - t0
+
+    def finish(pend):
+        slot, ev, te = pend
+        t0 = time.perf_counter()
+        ev.synchronize()
+        t1 = time.perf_counter()
+        toks, blen, steps, rt, rs, rv = (h.numpy().copy() for h in pinned[slot])
+        t2 = time.perf_counter()
+        recs = records_by_utterance(rt, rs, rv)
+        second_pass_select(recs, i2w, lm, 1.5, 1.5)
+        t3 = time.perf_counter()
+        print(f"pipe: enqueue {1e3 * te:.2f} ms, wait {1e3 * (t1 - t0):.2f}, copy-out {1e3 * (t2 - t1):.2f}, "
+              f"host {1e3 * (t3 - t2):.2f} ms", flush=True)
+
+    if os.environ.get("FREEZE", "1") == "1":
+        import gc
+        gc.collect()
+        gc.freeze()
+    t0 = time.perf_counter()
+    prev = None
+    for i in range(6):
+        cur = enqueue(i % 2)
+        if prev is not None:
+            finish(prev)
+        prev = cur
+    finish(prev)
+    print(f"pipe: {1e3 * (time.perf_counter() - t0) / 6:.2f} ms per batch", flush=True)
     eng.profile(["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"])
     feat, flen = eng.features(fb, fr)
     eng.encode(feat, flen)
