@@ -173,7 +173,6 @@ struct casr_handle {
   bool s16_valid = false;           // the bound blob's s16 images are usable (Layout::info)
   DevBuf x16;                       // s16 row image of the current layer input [B*Tp][Kp]
   bool s16() const { return precision == CASR_PREC_S16X3 && s16_valid; }
-  int rec_capacity = 0;  // workgroups of rec_layer_kernel resident at once (CUs x blocks/CU)
   int B = 0, Tp = 0;
   bool encoded = false;
   float* enc_out = nullptr;  // out0 or out1
@@ -405,10 +404,6 @@ int casr_create(const casr_config* cfg, int device, casr_handle** out) {
   h->cfg = *cfg;
   h->L = make_layout(*cfg);
   h->device = device;
-  // the persistent recurrence needs every workgroup of its grid resident at once
-  int per_cu = 0;
-  if (hipSetDevice(device) == hipSuccess && rec_layer_occupancy(&per_cu) == hipSuccess)
-    h->rec_capacity = per_cu * prop.multiProcessorCount;
   *out = h;
   return CASR_OK;
 }
@@ -474,7 +469,9 @@ int casr_set_persistent(casr_handle* h, int enable) {
 
 int casr_recurrence_mode(const casr_handle* h, int B) {
   if (!h || B <= 0) return -1;
-  return (h->use_persistent && rec_layer_grid_blocks(B) <= h->rec_capacity) ? 1 : 0;
+  // the persistent recurrence needs every workgroup of its grid resident at once
+  if (!h->use_persistent || hipSetDevice(h->device) != hipSuccess) return 0;
+  return rec_layer_fits(B) ? 1 : 0;
 }
 
 const char* casr_last_error(const casr_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
@@ -612,7 +609,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
       // diagnostics only: CASR_REC_TRACE=<file> dumps per-wave phase timestamps of layer 0
       const char* trace_path = l == 0 ? std::getenv("CASR_REC_TRACE") : nullptr;
       DevBuf tbuf;
-      const size_t tbytes = (size_t)rec_layer_grid_blocks(B) * rec_layer_waves() * Tp * 5 * sizeof(uint32_t);
+      const size_t tbytes = (size_t)rec_layer_grid_blocks(B) * rec_layer_waves(B) * Tp * 5 * sizeof(uint32_t);
       if (trace_path) {
         HIP_OK(h, tbuf.ensure(tbytes));
         HIP_OK(h, hipMemsetAsync(tbuf.p, 0, tbytes, s));
@@ -632,7 +629,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
         HIP_OK(h, hipStreamSynchronize(s));
         tbuf.release();
         if (FILE* f = std::fopen(trace_path, "wb")) {
-          const int32_t hdr[5] = {rec_layer_grid_blocks(B), rec_layer_waves(), Tp, 5, rec_layer_producers()};
+          const int32_t hdr[5] = {rec_layer_grid_blocks(B), rec_layer_waves(B), Tp, 5, rec_layer_producers(B)};
           std::fwrite(hdr, sizeof hdr, 1, f);
           std::fwrite(hostv.data(), 4, hostv.size(), f);
           std::fclose(f);

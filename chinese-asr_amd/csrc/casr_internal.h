@@ -199,9 +199,9 @@ hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xi
 // recurrence.hip: persistent per-layer recurrence (all Tp steps in one launch)
 size_t rec_layer_granule_bytes(int B);
 int rec_layer_grid_blocks(int B);
-int rec_layer_waves();  // waves per workgroup (trace layout)
-int rec_layer_producers();  // workgroups per row group (trace layout)
-hipError_t rec_layer_occupancy(int* blocks_per_cu);
+int rec_layer_waves(int B);  // waves per workgroup (trace layout)
+int rec_layer_producers(int B);  // workgroups per row group (trace layout)
+bool rec_layer_fits(int B);  // the persistent grid for batch B is resident at once (one launch)
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s);  // before EVERY launch_rec_layer
 // x16 (s16 only, may be null): also write out's s16 row image [B*Tp][C/32][32 hi | 32 lo] (the
 // next layer's input-GEMM operand, zeros past each length), replacing a split_rows pass

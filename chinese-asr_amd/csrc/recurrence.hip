@@ -463,17 +463,32 @@ static int rec_poll_gap() {
   return v;
 }
 
-static int rec_layout() {
+// CUs of the current device (the persistent grid wants one workgroup per CU)
+static int rec_cus() {
   static const int v = [] {
-    const char* e = std::getenv("CASR_REC_LAYOUT");
-    if (e && strcmp(e, "16x32") == 0) return 1;
-    if (e && strcmp(e, "16x16") == 0) return 2;
-    return 0;
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
   }();
   return v;
 }
-static int rec_rows() { return rec_layout() == 0 ? 32 : 16; }
-static int rec_units() { return rec_layout() == 1 ? 32 : 16; }
+
+// Layout per batch.  32x16 (512 threads: 32 rows x 16 units) while its grid of 16 x ceil(B/32) x 2
+// workgroups needs all the CUs (B = 256: one per CU); 16x16 (256 threads) once 16 x ceil(B/16) x 2
+// workgroups still fit one per CU (B <= 128): twice the workgroups, each with half the rows, so
+// a step's MFMA and cell work per CU halves while the hand-off stays a 16-producer exchange.
+// Measured (rec ms per batch, two interleaved rounds): beam B = 128 2.36-2.37 (32x16) -> 2.01-2.02
+// (16x16); greedy B = 256 2.67-2.71 (32x16) vs 3.08-3.10 (16x16: two workgroups per CU).
+// CASR_REC_LAYOUT = 32x16 / 16x32 / 16x16 forces one (tuning knob; read at every call, so a test
+// can run both layouts in one process).
+static int rec_layout(int B) {
+  const char* e = std::getenv("CASR_REC_LAYOUT");
+  if (e) return strcmp(e, "16x32") == 0 ? 1 : strcmp(e, "16x16") == 0 ? 2 : 0;
+  return (H / 16) * ((B + 15) / 16) * 2 <= rec_cus() ? 2 : 0;
+}
+static int rec_rows(int B) { return rec_layout(B) == 0 ? 32 : 16; }
+static int rec_units(int B) { return rec_layout(B) == 1 ? 32 : 16; }
 
 // the three granule buffers, then the placement table (one word per workgroup)
 static size_t rec_granule_words(int B) { return (size_t)3 * 2 * ((B + 31) / 32 * 32) * H; }
@@ -482,28 +497,33 @@ size_t rec_layer_granule_bytes(int B) {
   return (rec_granule_words(B) + (size_t)rec_layer_grid_blocks(B)) * sizeof(uint32_t);
 }
 
-int rec_layer_waves() { return rec_rows() * rec_units() / 64; }
+int rec_layer_waves(int B) { return rec_rows(B) * rec_units(B) / 64; }
 
-int rec_layer_producers() { return H / rec_units(); }
+int rec_layer_producers(int B) { return H / rec_units(B); }
 
-int rec_layer_grid_blocks(int B) { return (H / rec_units()) * ((B + rec_rows() - 1) / rec_rows()) * 2; }
+int rec_layer_grid_blocks(int B) { return (H / rec_units(B)) * ((B + rec_rows(B) - 1) / rec_rows(B)) * 2; }
 
 template <int RG, int UW>
-static hipError_t occ(int* n) {
+static int occ() {
   // both arithmetic variants must fit: the capacity is the smaller of the two
-  int a = 0, b = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rec_layer_kernel<RG, UW, false>, RG * UW, 0);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rec_layer_kernel<RG, UW, true>, RG * UW, 0);
-  *n = a < b ? a : b;
-  return e;
+  static const int v = [] {
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, rec_layer_kernel<RG, UW, false>, RG * UW, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, rec_layer_kernel<RG, UW, true>, RG * UW, 0) != hipSuccess)
+      return 0;
+    return a < b ? a : b;
+  }();
+  return v;
 }
 
-hipError_t rec_layer_occupancy(int* blocks_per_cu) {
-  switch (rec_layout()) {
-    case 1: return occ<16, 32>(blocks_per_cu);
-    case 2: return occ<16, 16>(blocks_per_cu);
-    default: return occ<32, 16>(blocks_per_cu);
+bool rec_layer_fits(int B) {
+  int per_cu;
+  switch (rec_layout(B)) {
+    case 1: per_cu = occ<16, 32>(); break;
+    case 2: per_cu = occ<16, 16>(); break;
+    default: per_cu = occ<32, 16>(); break;
   }
+  return rec_layer_grid_blocks(B) <= per_cu * rec_cus();
 }
 
 hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
@@ -520,7 +540,7 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
                             uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s) {
   const int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for every layout
-  const int RG = rec_rows(), UW = rec_units();
+  const int RG = rec_rows(B), UW = rec_units(B);
   const int nrg = (B + RG - 1) / RG;
   dim3 grid((H / UW) * nrg * 2);
   auto go = [&](auto kern) {
@@ -528,7 +548,7 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
                        residual, err, trace, nrg, rec_pre_wait(), rec_pre_sleep(), rec_poll_gap(),
                        rec_store_plain());
   };
-  switch (rec_layout()) {
+  switch (rec_layout(B)) {
     case 1: s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>); break;
     case 2: s16 ? go(rec_layer_kernel<16, 16, true>) : go(rec_layer_kernel<16, 16, false>); break;
     default: s16 ? go(rec_layer_kernel<32, 16, true>) : go(rec_layer_kernel<32, 16, false>); break;

@@ -254,11 +254,14 @@ def test_fused_select_equals_select_launches(eng, eos_bias):
         assert bool(outs[1]["finished"].any()), "with the EOS bias some rows must finish early"
 
 
-@pytest.mark.parametrize("B", [37, 256])
-def test_persistent_recurrence_equals_per_step(eng, B):
+@pytest.mark.parametrize("B,layout", [(37, None), (37, "32x16"), (256, None)])
+def test_persistent_recurrence_equals_per_step(eng, B, layout, monkeypatch):
     """The persistent per-layer recurrence (granule hand-offs, either store flavour) and the
     per-step launches give bitwise-identical encoder outputs and final states, on ragged lengths (B = 37: a partial
-    32-row group and padding rows; B = 256: the full 256-workgroup grid)."""
+    row group and padding rows, in the 16x16 layout the batch selects and in the forced 32x16 one;
+    B = 256: the full 256-workgroup grid of 32x16)."""
+    if layout:
+        monkeypatch.setenv("CASR_REC_LAYOUT", layout)
     enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
     eng.bind(pack_weights(CFG, enc_sd, dec_sd))
     rs = np.random.RandomState(11)
