@@ -45,18 +45,22 @@ struct Order16 {
   }
 };
 
-template <int WN>  // waves along N: 2 -> 4 waves of 128 x 128, 4 -> 8 waves of 128 x 64
-__global__ __launch_bounds__(128 * WN, WN / 2) void gemm16_bias_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
+// WN: waves along N (2 -> 128 x 128 wave tiles, 4 -> 128 x 64); MH: 128-row halves of the tile
+// (2: 256 x 256 with 2 WN waves; 1: 128 x 256 with WN waves, the half tiles that balance the
+// persistent kernel's last round, launch_input_proj_s16_big)
+template <int WN, int MH = 2>
+__global__ __launch_bounds__(64 * MH * WN, WN* MH / 4) void gemm16_bias_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
                                                           const float* __restrict__ bias, float* __restrict__ Cout,
                                                           int M, int N, int Kp, Order16 order) {
-  __shared__ __attribute__((aligned(16))) float buf0[2 * G16_TILE];  // [A tile | W tile]
-  __shared__ __attribute__((aligned(16))) float buf1[2 * G16_TILE];
+  constexpr int BM = 128 * MH, ATILE = BM * G16_K, NWV = MH * WN;
+  __shared__ __attribute__((aligned(16))) float buf0[ATILE + G16_TILE];  // [A tile | W tile]
+  __shared__ __attribute__((aligned(16))) float buf1[ATILE + G16_TILE];
   int nt, mt;
   if (!order.tile(blockIdx.x, nt, mt)) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NT = 8 / WN;                 // 32-column MFMA tiles per wave
   const int wm = wave / WN, wn = wave % WN;  // wave tile: rows [128 wm, +128) x columns [32 NT wn, +32 NT)
-  const int m0 = mt * G16_M, n0 = nt * G16_N;
+  const int m0 = mt * BM, n0 = nt * G16_N;
 
   // wave tile 128 x 128 as 4 x 4 tiles of v_mfma_f32_32x32x16_f16 (16 accumulators each):
   // lane l holds A[row l&31][k = 16s + 8(l>>5) + j] and B[k][col l&31] (j = 0..7) for k-step s,
@@ -70,24 +74,30 @@ __global__ __launch_bounds__(128 * WN, WN / 2) void gemm16_bias_kernel(const flo
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
   const int r32 = lane & 31, hsel = lane >> 5;
 
-  // wave w stages rows [RW w, RW w + RW) of both tiles: RW/8 + RW/8 DMA instructions of 8 rows x 128 B
-  constexpr int RW = 256 / (2 * WN);
+  // wave w stages A rows [RWA w, +RWA) and W rows [RWW w, +RWW): DMA instructions of 8 rows x 128 B
+  constexpr int RWA = BM / NWV, RWW = G16_N / NWV;
   auto stage = [&](float* dst, int k0) {
 #pragma unroll
-    for (int i = 0; i < RW / 8; ++i) {
-      const int row = wave * RW + i * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
-      const int ar = min(m0 + row, M - 1), wr = min(n0 + row, N - 1);
-      float* la = dst + (wave * RW + i * 8) * G16_K;
+    for (int i = 0; i < RWA / 8; ++i) {
+      const int row = wave * RWA + i * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+      const int ar = min(m0 + row, M - 1);
+      float* la = dst + (wave * RWA + i * 8) * G16_K;
       __builtin_amdgcn_global_load_lds(A16 + (size_t)ar * Kp + k0 + c * 4,
                                        (__attribute__((address_space(3))) void*)la, 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < RWW / 8; ++i) {
+      const int row = wave * RWW + i * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+      const int wr = min(n0 + row, N - 1);
+      float* lw = dst + ATILE + (wave * RWW + i * 8) * G16_K;
       __builtin_amdgcn_global_load_lds(W16 + (size_t)wr * Kp + k0 + c * 4,
-                                       (__attribute__((address_space(3))) void*)(la + G16_TILE), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)lw, 16, 0, 0);
     }
   };
   const _Float16 two11 = (_Float16)2048.0f;
   auto compute = [&](const float* src) {
     const float* as = src;
-    const float* ws = src + G16_TILE;
+    const float* ws = src + ATILE;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = 2 * ks + hsel;  // 16-B chunk of this lane's 8 k (hi); lo is chunk 4 + ch
@@ -130,12 +140,12 @@ __global__ __launch_bounds__(128 * WN, WN / 2) void gemm16_bias_kernel(const flo
 
   // epilogue: eight 32-row slabs staged through LDS (buf0), stored as whole 1 KB rows
   constexpr int LDC = G16_N + 4;
-  static_assert(32 * LDC <= 2 * G16_TILE, "slab fits one stage buffer");
-  const int c4 = tid & 63, r0 = tid >> 6;  // 64 float4 per row, 2 WN rows per pass
+  static_assert(32 * LDC <= ATILE + G16_TILE, "slab fits one stage buffer");
+  const int c4 = tid & 63, r0 = tid >> 6;  // 64 float4 per row, NWV rows per pass
   const int col = n0 + c4 * 4;
   const float4 b4 = col < N ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int p = 0; p < 8; ++p) {
+  for (int p = 0; p < 4 * MH; ++p) {
     // slab p = rows [32p, 32p + 32) = tile tm = p & 3 of the waves with wm = p >> 2
     if (wm == (p >> 2)) {
 #pragma unroll
@@ -147,7 +157,7 @@ __global__ __launch_bounds__(128 * WN, WN / 2) void gemm16_bias_kernel(const flo
     __syncthreads();
     if (col < N) {
 #pragma unroll
-      for (int row = r0; row < 32; row += 2 * WN) {
+      for (int row = r0; row < 32; row += NWV) {
         const int gr = m0 + p * 32 + row;
         if (gr >= M) break;
         const float4 v = *reinterpret_cast<const float4*>(buf0 + row * LDC + c4 * 4);
@@ -365,13 +375,16 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
 
 }  // namespace
 
-// CASR_GEMM16_PERSIST: 1 (default) = gemm16_persist_kernel, 0 = gemm16_bias_kernel (A/B knob)
+// CASR_GEMM16_PERSIST: 1 (default) = gemm16_persist_kernel, 0 = gemm16_bias_kernel (A/B knob,
+// read at every launch so a test can compare both); CASR_GEMM16_TAIL=0 keeps the persistent
+// kernel's partial last round instead of the half-tile tail launch
 static bool gemm16_persist() {
-  static const bool v = [] {
-    const char* e = std::getenv("CASR_GEMM16_PERSIST");
-    return !e || std::atoi(e) != 0;
-  }();
-  return v;
+  const char* e = std::getenv("CASR_GEMM16_PERSIST");
+  return !e || std::atoi(e) != 0;
+}
+static bool gemm16_tail() {
+  const char* e = std::getenv("CASR_GEMM16_TAIL");
+  return !e || std::atoi(e) != 0;
 }
 
 // CASR_GEMM16_WAVES: 8 (default) or 4 waves per 256 x 256 tile; 0 = encoder.hip's 128 x 128
@@ -401,12 +414,34 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
       (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
       return v > 0 ? v : 256;
     }();
-    const int total = order.blocks();
     // the persistent kernel runs ceil(K / 32) stages of the Kp-wide images (both zero past K): layer
     // 0 (K = 720, Kp = 768) skips the all-zero last stage
     const int nk = (K > 0 && K <= Kp ? K + G16_K - 1 : Kp) / G16_K;
+    // Balanced last round.  NB x NM tiles over ncu workgroups leave a partial last round (B = 256:
+    // 2128 tiles = 8 rounds + 80 tiles, so 80 CUs run a ninth tile while 176 idle; B = 128: 4
+    // rounds + 40).  The persistent kernel takes the first F = floor(NB NM / ncu) rounds (whole row
+    // tiles: F ncu / NB of them, every workgroup exactly F tiles) and the rows after them go to
+    // one launch of 128 x 256 half tiles (gemm16_bias_kernel<4, 1>, one per CU), which run at one
+    // wave per SIMD.  Same per-element arithmetic as the persistent kernel: bitwise equal.
+    int NMm = NM;
+    const int F = NB * NM / ncu;
+    if (gemm16_tail() && F >= 1 && (F * ncu) % NB == 0 && F * ncu / NB < NM) {
+      const int nm = F * ncu / NB;
+      const int tail_rows = M - nm * G16_M, NMt = (tail_rows + 127) / 128;
+      if (NB * NMt <= ncu) NMm = nm;  // the half tiles fit one round
+    }
+    const Order16 om{NB, NMm, NG};
+    const int total = om.blocks();
     hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
-                       M, N, Kp, order, total, nk);
+                       std::min(M, NMm * G16_M), N, Kp, om, total, nk);
+    if (NMm < NM) {
+      const size_t r0 = (size_t)NMm * G16_M;
+      const int Mt = M - (int)r0, NMt = (Mt + 127) / 128;
+      int NGt = NG;  // XCD grouping of the tail: the same column slices per XCD as the main part
+      const Order16 ot{NB, NMt, NGt};
+      hipLaunchKernelGGL((gemm16_bias_kernel<4, 1>), dim3(ot.blocks()), dim3(256), 0, s, X16 + r0 * Kp, W16, bias,
+                         Gin + r0 * N, Mt, N, Kp, ot);
+    }
   } else if (gemm16_waves() == 8)
     hipLaunchKernelGGL(gemm16_bias_kernel<4>, dim3(order.blocks()), dim3(512), 0, s, X16, W16, bias, Gin, M, N, Kp,
                        order);

@@ -473,3 +473,29 @@ def test_model_reruns_f32_on_f16_range_overflow():
     m.engine.set_precision("s16x3")
     assert g.pred_text == g32.pred_text
     np.testing.assert_array_equal(np.asarray(g.score), np.asarray(g32.score))
+
+
+@pytest.mark.parametrize("B", [256, 128, 37])
+def test_input_gemm_tail_split_bitwise(eng, B, monkeypatch):
+    """s16x3 input projection: the persistent kernel over whole rounds plus the 128 x 256 half-tile
+    launch for the rows after them (default), the persistent kernel alone (CASR_GEMM16_TAIL=0) and
+    the per-tile kernel (CASR_GEMM16_PERSIST=0) give bitwise-identical encoder outputs (B = 256
+    and 128: 80 / 40 tiles past the last whole round; B = 37: 48 tiles in one partial round)."""
+    if eng.precision() != "s16x3":
+        pytest.skip("the split-f16 input GEMM only")
+    bind(eng, "peaked")
+    rs = np.random.RandomState(5)
+    frames = [800] * (B - 2) + [int(rs.randint(9, 800)), 9]
+    fb, fr = batch_fbank(frames, eng.device)
+    outs = []
+    for env in ({}, {"CASR_GEMM16_TAIL": "0"}, {"CASR_GEMM16_PERSIST": "0"}):
+        for k in ("CASR_GEMM16_TAIL", "CASR_GEMM16_PERSIST"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        eng.encode_fbank(fb, fr)
+        assert eng.device_flags() == 0
+        outs.append([t.cpu() for t in eng.encoder_results()])
+    for got in outs[1:]:
+        for a, b in zip(outs[0], got):
+            assert torch.equal(a, b)
