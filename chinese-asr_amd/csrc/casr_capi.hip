@@ -842,11 +842,13 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   dg_trace_init();  // CASR_DG_TRACE diagnostics only (outside any capture)
   HIP_OK(h, run_graph(h, key, s, [&](hipStream_t cs) { return run_greedy(a, h->d, itok, ilen, ifin, iacc, ial, cs); }));
   dg_trace_dump();  // CASR_DG_TRACE diagnostics only (no-op otherwise)
-  HIP_OK(h, hipMemcpyAsync(tokens, itok, sizeof(int32_t) * B * L, hipMemcpyDeviceToDevice, s));
-  HIP_OK(h, hipMemcpyAsync(out_len, ilen, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
-  HIP_OK(h, hipMemcpyAsync(finished, ifin, B, hipMemcpyDeviceToDevice, s));
-  HIP_OK(h, hipMemcpyAsync(accum, iacc, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
-  if (align) HIP_OK(h, hipMemcpyAsync(align, ial, sizeof(float) * nal, hipMemcpyDeviceToDevice, s));
+  CopyList cl;  // the graph's outputs to the caller's buffers in one launch
+  cl.add(tokens, itok, sizeof(int32_t) * B * L);
+  cl.add(out_len, ilen, sizeof(int32_t) * B);
+  cl.add(finished, ifin, B);
+  cl.add(accum, iacc, sizeof(float) * B);
+  if (align) cl.add(align, ial, sizeof(float) * nal);
+  HIP_OK(h, copy_multi(cl, s));
   return CASR_OK;
 }
 
@@ -885,10 +887,12 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
     return run_beam(a, h->d, lm_weight, length_weight, itok, ilen, isc, istp, cs);
   }));
   dg_trace_dump();
-  HIP_OK(h, hipMemcpyAsync(best_tokens, itok, sizeof(int32_t) * B * L, hipMemcpyDeviceToDevice, s));
-  HIP_OK(h, hipMemcpyAsync(best_len, ilen, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
-  HIP_OK(h, hipMemcpyAsync(best_score, isc, sizeof(float) * B, hipMemcpyDeviceToDevice, s));
-  HIP_OK(h, hipMemcpyAsync(steps, istp, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+  CopyList cl;  // the graph's outputs to the caller's buffers in one launch
+  cl.add(best_tokens, itok, sizeof(int32_t) * B * L);
+  cl.add(best_len, ilen, sizeof(int32_t) * B);
+  cl.add(best_score, isc, sizeof(float) * B);
+  cl.add(steps, istp, sizeof(int32_t));
+  HIP_OK(h, copy_multi(cl, s));
   return CASR_OK;
 }
 

@@ -151,6 +151,32 @@ struct GraphCache {
 // fill.hip (graph-safe replacements for hipMemsetAsync)
 hipError_t fill_u32(void* p, uint32_t v, size_t n_words, hipStream_t s);
 hipError_t fill_u8(void* p, uint8_t v, size_t n_bytes, hipStream_t s);
+// up to FILL_MAX_SEG fills (4-byte words or bytes) / device-to-device copies in one launch
+constexpr int FILL_MAX_SEG = 8;
+struct FillSeg {
+  void* p;
+  size_t count;    // elements
+  uint32_t v;
+  uint32_t bytes;  // element size: 4 or 1
+};
+struct FillList {
+  FillSeg seg[FILL_MAX_SEG];
+  int n = 0;
+  void add32(void* p, uint32_t v, size_t n_words) { seg[n++] = FillSeg{p, n_words, v, 4}; }
+  void add8(void* p, uint8_t v, size_t n_bytes) { seg[n++] = FillSeg{p, n_bytes, v, 1}; }
+};
+hipError_t fill_multi(const FillList& fl, hipStream_t s);
+struct CopySeg {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+struct CopyList {
+  CopySeg seg[FILL_MAX_SEG];
+  int n = 0;
+  void add(void* dst, const void* src, size_t bytes) { seg[n++] = CopySeg{dst, src, bytes}; }
+};
+hipError_t copy_multi(const CopyList& cl, hipStream_t s);
 
 // frontend.hip: wav -> log-mel.  Constant tables live in one device struct per handle.
 struct FrontendConst {

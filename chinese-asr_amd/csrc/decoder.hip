@@ -1581,12 +1581,14 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
   a.greedy_run = 1;
   const int R = a.B;
   // fill kernels, not hipMemsetAsync: this sequence is captured into a replayed graph
-  hipError_t e0 = fill_u32(d.newdone, 0, a.max_len, s);
-  if (e0 == hipSuccess) e0 = fill_u32(d.err, 0, 1, s);
-  if (e0 == hipSuccess) e0 = fill_u8(finished, 0, R, s);
-  if (e0 == hipSuccess) e0 = fill_u32(out_len, 0, R, s);
-  if (e0 == hipSuccess) e0 = fill_u32(accum, 0, R, s);
-  if (e0 == hipSuccess) e0 = fill_u32(tokens, 0xffffffffu, (size_t)R * a.max_len, s);
+  FillList fl;
+  fl.add32(d.newdone, 0, a.max_len);
+  fl.add32(d.err, 0, 1);
+  fl.add8(finished, 0, R);
+  fl.add32(out_len, 0, R);
+  fl.add32(accum, 0, R);
+  fl.add32(tokens, 0xffffffffu, (size_t)R * a.max_len);
+  hipError_t e0 = fill_multi(fl, s);
   if (e0 != hipSuccess) return e0;
   // the select of step l runs inside step l+1's LSTMCell (GreedySel) when the projection writes
   // per-block partials; the last step's select is a launch of its own.  CASR_FUSE_SELECT=0 keeps
@@ -1631,9 +1633,11 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
                     int32_t* best_tokens, int32_t* best_len, float* best_score, int32_t* steps,
                     hipStream_t s) {
   const int R = a.B * a.k;
-  hipError_t e0 = fill_u32(d.newdone, 0, a.max_len, s);
-  if (e0 == hipSuccess) e0 = fill_u32(d.err, 0, 1, s);
-  if (e0 == hipSuccess) e0 = fill_u8(d.topfin, 0, a.B, s);
+  FillList fl;
+  fl.add32(d.newdone, 0, a.max_len);
+  fl.add32(d.err, 0, 1);
+  fl.add8(d.topfin, 0, a.B);
+  hipError_t e0 = fill_multi(fl, s);
   if (e0 != hipSuccess) return e0;
   hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, a.k,
                      a.sos, d.tok[0], d.src[0], d.score[0], nullptr);

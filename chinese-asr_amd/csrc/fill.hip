@@ -30,4 +30,53 @@ hipError_t fill_u8(void* p, uint8_t v, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Several fills / copies in one launch (blockIdx.y = segment): the small per-call resets of the
+// recurrence hand-off buffers and of the decode state, and the copies of a decode graph's outputs
+// to the caller's buffers, were one launch each (≈5 µs apiece on the profile's timeline).
+__global__ void fill_multi_kernel(FillList fl) {
+  const FillSeg sg = fl.seg[blockIdx.y];
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  if (sg.bytes == 4) {
+    uint32_t* p = reinterpret_cast<uint32_t*>(sg.p);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.count; i += step) p[i] = sg.v;
+  } else {
+    uint8_t* p = reinterpret_cast<uint8_t*>(sg.p);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.count; i += step) p[i] = (uint8_t)sg.v;
+  }
+}
+
+hipError_t fill_multi(const FillList& fl, hipStream_t s) {
+  if (fl.n <= 0 || fl.n > FILL_MAX_SEG) return hipErrorInvalidValue;
+  size_t mx = 0;
+  for (int i = 0; i < fl.n; ++i) mx = std::max(mx, fl.seg[i].count);
+  if (mx == 0) return hipSuccess;
+  const unsigned blocks = (unsigned)std::min<size_t>((mx + 255) / 256, 1024);
+  hipLaunchKernelGGL(fill_multi_kernel, dim3(blocks, fl.n), dim3(256), 0, s, fl);
+  return hipGetLastError();
+}
+
+__global__ void copy_multi_kernel(CopyList cl) {
+  const CopySeg sg = cl.seg[blockIdx.y];
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  const bool w4 = ((reinterpret_cast<uintptr_t>(sg.dst) | reinterpret_cast<uintptr_t>(sg.src) | sg.bytes) & 3) == 0;
+  if (w4) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(sg.dst);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(sg.src);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.bytes / 4; i += step) d[i] = q[i];
+  } else {
+    uint8_t* d = reinterpret_cast<uint8_t*>(sg.dst);
+    const uint8_t* q = reinterpret_cast<const uint8_t*>(sg.src);
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.bytes; i += step) d[i] = q[i];
+  }
+}
+
+hipError_t copy_multi(const CopyList& cl, hipStream_t s) {
+  if (cl.n <= 0 || cl.n > FILL_MAX_SEG) return hipErrorInvalidValue;
+  size_t mx = 0;
+  for (int i = 0; i < cl.n; ++i) mx = std::max(mx, cl.seg[i].bytes / 4 + 1);
+  const unsigned blocks = (unsigned)std::min<size_t>((mx + 255) / 256, 1024);
+  hipLaunchKernelGGL(copy_multi_kernel, dim3(blocks, cl.n), dim3(256), 0, s, cl);
+  return hipGetLastError();
+}
+
 }  // namespace casr

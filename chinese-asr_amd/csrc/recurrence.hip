@@ -531,9 +531,11 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
   // (j = 0), expecting parity 1, 0, 1: fill buffers 0 and 1 with parity 0, buffer 2 with 1.
   // The placement table after them starts at 0 (no id published).
   const size_t per = rec_granule_words(B) / 3;
-  hipError_t e = fill_u32(hx, 0u, 2 * per, s);
-  if (e == hipSuccess) e = fill_u32(hx + 2 * per, TAG_BIT, per, s);
-  return e == hipSuccess ? fill_u32(hx + 3 * per, 0u, (size_t)rec_layer_grid_blocks(B), s) : e;
+  FillList fl;
+  fl.add32(hx, 0u, 2 * per);
+  fl.add32(hx + 2 * per, TAG_BIT, per);
+  fl.add32(hx + 3 * per, 0u, (size_t)rec_layer_grid_blocks(B));
+  return fill_multi(fl, s);
 }
 
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
