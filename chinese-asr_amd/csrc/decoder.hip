@@ -306,14 +306,21 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   }
   // k slices 1..KQ-1 hand their partial sums to slice 0 through LDS (the ring is free now)
   if constexpr (KQ > 1) {
-    f32x4* part = reinterpret_cast<f32x4*>(lb0);
-    static_assert((KQ - 1) * WR * WC * RS * NTW * 64 * 16 <= STG * 4, "partials fit one stage buffer");
-    auto slot = [&](int j, int rs, int tn) { return ((((j * WR + ws) * WC + wc) * RS + rs) * NTW + tn) * 64 + lane; };
+    // partial slots in lb0, continued in lb2 when they outgrow one stage buffer (32-row
+    // projection blocks: 3 x 2 x 5 tiles); the epilogue below uses lb1 (and lb0 for waves >= 4)
+    constexpr int CAP = STG * 4 / 16, NPART = (KQ - 1) * WR * WC * RS * NTW * 64;
+    static_assert(NPART <= CAP || (S > 2 && NPART <= 2 * CAP), "partials fit lb0 (+ lb2)");
+    static_assert(NPART <= CAP || WR * WC <= 4, "with lb2 in use the epilogue waves stay on lb1");
+    auto part = [&](int j, int rs, int tn) -> f32x4& {
+      const int i = ((((j * WR + ws) * WC + wc) * RS + rs) * NTW + tn) * 64 + lane;
+      if constexpr (NPART <= CAP) return reinterpret_cast<f32x4*>(lb0)[i];
+      else return i < CAP ? reinterpret_cast<f32x4*>(lb0)[i] : reinterpret_cast<f32x4*>(lb2)[i - CAP];
+    };
     if (kq > 0) {
 #pragma unroll
       for (int rs = 0; rs < RS; ++rs)
 #pragma unroll
-        for (int tn = 0; tn < NTW; ++tn) part[slot(kq - 1, rs, tn)] = acc[rs][tn];
+        for (int tn = 0; tn < NTW; ++tn) part(kq - 1, rs, tn) = acc[rs][tn];
     }
     __syncthreads();
     if (kq > 0) return;
@@ -322,7 +329,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
 #pragma unroll
       for (int rs = 0; rs < RS; ++rs)
 #pragma unroll
-        for (int tn = 0; tn < NTW; ++tn) acc[rs][tn] += part[slot(j, rs, tn)];
+        for (int tn = 0; tn < NTW; ++tn) acc[rs][tn] += part(j, rs, tn);
   }
   // lane holds rows erow0(rs) + e (e = 0..3), column (nbw*NTW + tn)*16 + r
   // per-wave LDS scratch for the epilogue (ring buffers are free now; the k-slice exchange
@@ -1494,7 +1501,9 @@ template <class ASrc, class Epi>
 static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi, int s16,
                         hipStream_t s) {
   const int nkt = KPROJ / DG_BK, NB = (ntiles + 4) / 5;  // 5 column tiles per block (10 at R > 512)
-  if (R <= 256) launch_dg<4, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  // R <= 32 (BASELINE config 2): 32-row blocks, so no block stages and multiplies 32 padding rows
+  if (R <= 32) launch_dg<2, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else if (R <= 256) launch_dg<4, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 512) launch_dg<8, 5, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else launch_dg<4, 10, 2, 2, 2, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
