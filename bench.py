@@ -287,6 +287,31 @@ def main():
         small = {"config": "BASELINE config 2: greedy, B=32/GPU, T=800", "batch_per_gpu": Bs,
                  "value": Bs * world * args.steps / dts, "unit": "utt/s", "ms_per_step": 1000.0 * dts / args.steps}
 
+    # BASELINE config 1: one 8 s WAV, greedy, through the drop-in main.parse (main.py:27-65):
+    # 16 kHz samples on the host -> log-mel, delta / stack / CMVN -> encoder -> greedy -> text.
+    # A latency: one utterance per call, the host-side Python of the reference's entry point
+    # included (the reference runs this case on the CPU).
+    single = None
+    if not args.no_configs and rank == 0:
+        import main as casr_main
+        import model as casr_model
+        from data import AudioBase
+        m1 = casr_model.Model()
+        m1.load_state_dicts(*synthetic_state_dicts(cfg, peaked=True, eos_bias=0.0))
+        ab = AudioBase()
+        wav = (0.1 * np.random.RandomState(99).standard_normal(int(AUDIO_S_PER_UTT * 16000) + 512)).astype(np.float32)
+        text = casr_main.parse(wav, m1, ab, None, None)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        n1 = max(3, args.steps)
+        for _ in range(n1):
+            text = casr_main.parse(wav, m1, ab, None, None)
+        dt1 = (time.perf_counter() - t1) / n1
+        single = {"config": "BASELINE config 1: one 8 s WAV, greedy, via the drop-in main.parse (wav -> text)",
+                  "latency_ms": 1000.0 * dt1, "rtf": dt1 / AUDIO_S_PER_UTT, "value": 1.0 / dt1,
+                  "unit": "utt/s", "chars": len(text)}
+        del m1
+
     # BASELINE config 5: beam 16 + second-pass LM rescoring, B = 128 per GPU (1024 on 8 GPUs).
     # Weights with the EOS bias of the peaked recipe so hypotheses finish and the second pass has
     # candidates to rescore; KenLM is absent offline, so the LM is a deterministic stub scored on
@@ -403,6 +428,7 @@ def main():
                                      "hand-off latency + MFMA + cell (DESIGN.md 3.2)"}
                             if dominant == "rec_step" else {})},
             "config2_greedy_b32": small,
+            "config1_single_wav": single,
             "config5_beam16_lm": lm_line,
             "f32_exact_path": f32_cmp,
             "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},
