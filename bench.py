@@ -132,7 +132,8 @@ def main():
     ap.add_argument("--no-beam", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the BASELINE config 2 (B=32 greedy) and config 5 (beam 16 + LM) side lines")
+                    help="skip the BASELINE config 1 (one WAV via main.parse), config 2 (B=32 greedy) and "
+                         "config 5 (beam 16 + LM) side lines")
     ap.add_argument("--cpu-sample", type=int, default=640)
     ap.add_argument("--precision", default="s16x3", choices=["s16x3", "f32"],
                     help="MFMA arithmetic of the timed path (casr_set_precision)")
