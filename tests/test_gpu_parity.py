@@ -499,3 +499,26 @@ def test_input_gemm_tail_split_bitwise(eng, B, monkeypatch):
     for got in outs[1:]:
         for a, b in zip(outs[0], got):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [1, 33, 129])
+def test_odd_batches_greedy_match_oracle(eng, B):
+    """Batch sizes at the layout boundaries, through casr_encode_fbank (T = 60, T' = 20, ragged
+    last utterance): B = 1 (one 16-row recurrence group, 32-row projection blocks, one attention
+    block), B = 33 (the 64-row projection blocks again, a partial 16-row group), B = 129 (the
+    recurrence back on 32 x 16 workgroups with a partial 32-row group).  Tokens identical to
+    the CPU oracle, scores within 2e-3."""
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    frames = [60] * (B - 1) + [33]
+    fb, fr = batch_fbank(frames, eng.device)
+    flen = eng.encode_fbank(fb, fr)
+    out = eng.greedy()
+    assert eng.device_flags() == 0
+    toks, score = greedy_outputs(out["tokens"].cpu().numpy(), out["out_len"].cpu().numpy(),
+                                 out["finished"].cpu().numpy().astype(bool), out["accum"].cpu().numpy())
+    feats = [O.features_from_fbank(fbank_for(b, t)) for b, t in enumerate(frames)]
+    assert flen.cpu().tolist() == [f.shape[0] for f in feats]
+    r = O.greedy_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd)
+    assert toks == r["tokens"]
+    np.testing.assert_allclose(score, r["score"], atol=2e-3, rtol=0)
