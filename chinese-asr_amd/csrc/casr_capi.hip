@@ -18,7 +18,7 @@ namespace casr {
 size_t attention_smem_bytes(int k, int Tp);  // decoder.hip
 
 // version word of the packed layout (bump whenever make_layout or a packer changes)
-constexpr uint32_t LAYOUT_MAGIC = 0xCA5B0002u;
+constexpr uint32_t LAYOUT_MAGIC = 0xCA5B0003u;
 
 Layout make_layout(const casr_config& cfg) {
   Layout L{};
@@ -330,7 +330,7 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
     for (int d = 0; d < 2; ++d)
       for (int g = 0; g < 4; ++g)
         for (int u = 0; u < H; ++u) {
-          const int pr = d * 4 * H + packed_gate_row(g, u);
+          const int pr = d * 4 * H + enc_gate_col(g, u);
           const int orow = g * H + u;
           std::memcpy(out + L.enc_wih[l] + (size_t)pr * din, w->enc_w_ih[l][d] + (size_t)orow * din,
                       sizeof(float) * din);

@@ -71,6 +71,10 @@ Layout make_layout(const casr_config& cfg);
 // Packed row index of (gate g, unit u) for a gate-interleaved LSTM matrix with hidden
 // size n_hidden: blocks of 16 units, each block = 4 gates x 16 units.
 inline int packed_gate_row(int g, int u) { return (u / 16) * 64 + g * 16 + (u % 16); }
+// Encoder input-projection column (Gin) of gate g of unit u within one direction: the four gates
+// of a unit are adjacent (16-unit blocks of [unit][gate]), so a recurrence cell reads its gate
+// pre-activations with one 16-B load instead of four 4-B loads (recurrence.hip, encoder.hip)
+inline int enc_gate_col(int g, int u) { return (u / 16) * 64 + (u % 16) * 4 + g; }
 
 // ---------------------------------------------------------------- launch timing
 // Event pairs around launches of enabled kernel classes (casr_profile_enable).

@@ -4,7 +4,7 @@
 //
 // Layout in HBM: batch-major rows (b*Tp + t).
 //   * input projection of a layer: one fp32 MFMA GEMM over all B*Tp rows for both
-//     directions, Gin[b*Tp+t][d*4H + packed(g,u)] = x . W_ih^T + (b_ih + b_hh)
+//     directions, Gin[b*Tp+t][d*4H + enc_gate_col(g,u)] = x . W_ih^T + (b_ih + b_hh)
 //     (128x128 LDS-tiled, v_mfma_f32_16x16x4_f32, exact f32);
 //   * recurrence: one launch per time step for both directions.  Each block owns
 //     16 batch rows x 16 hidden units (x 4 gates) of one direction; its 4 waves split the
@@ -385,9 +385,8 @@ __global__ __launch_bounds__(256) void rec_step_kernel(
   const size_t oi = ((size_t)b * Tp + t) * C + d * H + U;
   float gin_v[4] = {0.f, 0.f, 0.f, 0.f}, c_old = 0.f, x_res = 0.f;
   if (act) {
-    const float* gin = Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + jb * 64;
-#pragma unroll
-    for (int tn = 0; tn < 4; ++tn) gin_v[tn] = gin[tn * 16 + u];
+    const float4 q = *reinterpret_cast<const float4*>(Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + U * 4);
+    gin_v[0] = q.x, gin_v[1] = q.y, gin_v[2] = q.z, gin_v[3] = q.w;  // enc_gate_col: adjacent gates
     c_old = cst[si];
     if (residual) x_res = xin[oi];
   }

@@ -201,9 +201,9 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   auto load_operands = [&](int s, float (&g)[4], float& xr) {
     if (s < len) {
       const int t = (d == 0) ? s : (len - 1 - s);
-      const float* gp = Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + (U >> 4) * 64;
-#pragma unroll
-      for (int tn = 0; tn < 4; ++tn) g[tn] = gp[tn * 16 + (U & 15)];
+      // the cell's four gates are adjacent (casr_internal.h enc_gate_col): one 16-B load
+      const float4 q = *reinterpret_cast<const float4*>(Gin + ((size_t)b * Tp + t) * (8 * H) + d * 4 * H + U * 4);
+      g[0] = q.x, g[1] = q.y, g[2] = q.z, g[3] = q.w;
       if (residual) xr = xin[((size_t)b * Tp + t) * C + d * H + U];
     }
   };

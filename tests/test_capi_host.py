@@ -99,12 +99,12 @@ def test_packed_layout_contract():
     assert blob.size == lay["total"]
     rs = np.random.RandomState(0)
     H = 256
-    # encoder input projection rows: d*1024 + (u//16)*64 + g*16 + u%16 <- W_ih_d[g*H + u]
+    # encoder input projection rows: d*1024 + (u//16)*64 + (u%16)*4 + g <- W_ih_d[g*H + u]
     for l in (0, 2):
         din = 720 if l == 0 else 512
         for _ in range(20):
             d, g, u, k = rs.randint(2), rs.randint(4), rs.randint(H), rs.randint(din)
-            pr = d * 1024 + (u // 16) * 64 + g * 16 + u % 16
+            pr = d * 1024 + (u // 16) * 64 + (u % 16) * 4 + g
             suf = "_reverse" if d else ""
             W = enc[f"rnn.rnn.{l}.weight_ih_l0{suf}"]
             assert blob[lay[f"wih{l}"] + pr * din + k] == W[g * H + u, k]
@@ -200,7 +200,7 @@ def test_keys_weight_range_uses_f16_limit_and_layout_stamp():
     lay, total = _layout(CFG)
     assert blob[lay["info"]] == 1.0
     stamp = blob[lay["info"] + 1:lay["info"] + 4].view(np.uint32)
-    assert stamp[0] == 0xCA5B0002
+    assert stamp[0] == 0xCA5B0003
     assert int(stamp[1]) | (int(stamp[2]) << 32) == blob.size == L.packed_floats(CFG)
     w[7, 3] = 20000.0
     assert L.pack_weights(CFG, enc, dec)[lay["info"]] == 0.0

@@ -443,7 +443,7 @@ def test_bind_refuses_foreign_blob(eng):
     good = pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True))
     with pytest.raises(ValueError):
         eng.bind(torch.zeros(good.size + 64, dtype=torch.float32, device=eng.device))
-    at = np.nonzero(good.view(np.uint32) == 0xCA5B0002)[0]
+    at = np.nonzero(good.view(np.uint32) == 0xCA5B0003)[0]
     assert len(at) == 1  # the layout stamp's magic word
     bad = torch.from_numpy(good.copy()).to(eng.device)
     bad.view(torch.int32)[int(at[0])] = 0
