@@ -550,9 +550,13 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
     HIP_OK(h, hipMemsetAsync(h->out0.p, 0, rows * C * sizeof(float), s));
     HIP_OK(h, hipMemsetAsync(h->out1.p, 0, rows * C * sizeof(float), s));
   }
-  HIP_OK(h, hipMemsetAsync(h->hfin.p, 0, (size_t)2 * B * H * sizeof(float), s));
   HIP_OK(h, h->eflag.ensure(16));
-  HIP_OK(h, hipMemsetAsync(h->eflag.p, 0, 16, s));
+  {  // final h and the encoder guard words: one launch
+    FillList fl;
+    fl.add32(h->hfin.p, 0u, (size_t)2 * B * H);
+    fl.add32(h->eflag.p, 0u, 4);
+    HIP_OK(h, fill_multi(fl, s));
+  }
   const bool s16 = h->s16();
   if (s16) HIP_OK(h, h->x16.ensure(rows * s16_kpad(D) * sizeof(float)));
   if (persistent) HIP_OK(h, h->hx.ensure(rec_layer_granule_bytes(B)));

@@ -432,8 +432,14 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     }
     const Order16 om{NB, NMm, NG};
     const int total = om.blocks();
-    hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
-                       std::min(M, NMm * G16_M), N, Kp, om, total, nk);
+    // CASR_G16_IL=1: the interleaved stage-DMA variant (DIAG 32, A/B knob read at every launch)
+    const char* il = std::getenv("CASR_G16_IL");
+    if (il && std::atoi(il) != 0)
+      hipLaunchKernelGGL(gemm16_persist_kernel<32>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
+                         std::min(M, NMm * G16_M), N, Kp, om, total, nk);
+    else
+      hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
+                         std::min(M, NMm * G16_M), N, Kp, om, total, nk);
     if (NMm < NM) {
       const size_t r0 = (size_t)NMm * G16_M;
       const int Mt = M - (int)r0, NMt = (Mt + 127) / 128;
