@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """North-star benchmark: utterances/s (+ RTF) of the MI355X casr path on synthetic fbank of
-shape (B, T, F) = (256, 800, 80) per GPU, greedy decode (headline) and beam = 8 (B = 128).
+shape (B, T, F) = (256, 800, 80) per GPU, greedy decode (headline) and beam = 8 (the metric's
+beam line, B = 256; BASELINE config 3, B = 128, beside it).
 
 One step = features (delta/stack/CMVN, written straight as the encoder's layer-0 split-f16 image:
 casr_encode_fbank) -> 4-layer BiLSTM encoder -> attention keys -> 40-step decode loop -> token
@@ -8,6 +9,9 @@ ids copied to the host, for one batch per GPU.  Inputs are
 resident in HBM before the timed region.  Multi-GPU: one process per GPU (torchrun), rank 0
 packs the weights and RCCL-broadcasts the packed blob over xGMI; utterance batches are
 independent (no collective in the timed region except the start/stop barriers).
+`python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment) relaunches itself under
+torch.distributed.run with N ranks before touching the GPU; under a launcher, n_gpus is the live
+world size and a mismatch with --gpus is refused.
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
 """
@@ -15,6 +19,8 @@ import argparse
 import gc
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -76,8 +82,10 @@ LAUNCH_UNIT = {
 
 def kernel_bytes(cls, B, Tp, R, V):
     """Algorithmic HBM bytes of ONE launch of a kernel class (compulsory reads + writes), to set
-    beside the PMC-measured traffic; None where not tabulated."""
-    H, C, D, A = 256, 512, 720, 128
+    beside the PMC-measured traffic; None where not tabulated.  Weights are the s16 images (4 B
+    per element, like f32)."""
+    H, C, D, A, E, HD = 256, 512, 720, 128, 256, 512
+    VP = (V + 63) // 64 * 64
     if cls == "input_proj":  # average layer: X read, W_ih read, Gin written
         k = (D + 3 * C) / 4.0
         return 4.0 * (B * Tp * k + 8 * H * k + B * Tp * 8 * H)
@@ -85,6 +93,10 @@ def kernel_bytes(cls, B, Tp, R, V):
         return 4.0 * (B * Tp * 8 * H + B * Tp * C)
     if cls == "attention":
         return 4.0 * B * Tp * (A + C)
+    if cls == "dec_lstm":    # W image, the gathered A rows, new h / c / h16 and the query partials
+        return 4.0 * (4 * HD * (E + C + HD) + R * (E + C + HD) + 3 * R * HD + (HD // 16) * R * A)
+    if cls == "proj":        # W image, [ctx | h] rows, per-block (max, sum, argmax) partials
+        return 4.0 * (VP * (C + HD) + R * (C + HD) + 3 * R * 64)
     return None
 
 
@@ -97,26 +109,68 @@ class _StubLM:
         return -0.37 * len(ids) - 0.011 * sum(i % 97 for i in ids) - (0.5 if bos else 0.0)
 
 
-def cpu_baseline(n_utt, T):
-    """The CPU oracle (numpy restatement of the reference path, oracle/casr_oracle.py) timed
-    on this host on a bounded sample of the same workload."""
+# CPU port vs the reference itself on the same 8 container cores (tools/calibrate_cpu.py, committed
+# result profiles/r03/cpu_calibration.json): port utt/s / reference utt/s
+CPU_CALIBRATION = os.path.join(REPO, "profiles", "r03", "cpu_calibration.json")
+
+
+def cpu_baseline(n_utt, T, beam_k=0):
+    """The torch-CPU port of the reference path (oracle/torch_port.py: stock torch CPU operators,
+    nn.LSTM over packed sequences like the reference's RNN_RES; tokens equal to the reference
+    goldens, tests/test_torch_port.py) timed on this host's cores on a bounded sample of the same
+    workload: greedy (beam_k = 0) or beam beam_k.  Its speed relative to the reference itself on
+    the same cores was measured in the build container (profiles/r03/cpu_calibration.json)."""
     sys.path.insert(0, REPO)
-    from oracle import casr_oracle as O
+    from oracle import torch_port as TP
     from casr.config import CasrConfig
     from casr.weights import synthetic_state_dicts
     enc_sd, dec_sd = synthetic_state_dicts(CasrConfig(), peaked=True, eos_bias=0.0)
     fb = fbank_batch(0, n_utt, T)
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info()] + [1])
-    except Exception:
-        cores = os.cpu_count()
+    port = TP.TorchPort(enc_sd, dec_sd)
+    cores = torch.get_num_threads()
     t0 = time.perf_counter()
-    feats = [O.features_from_fbank(fb[b]) for b in range(n_utt)]
-    O.greedy_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd)
+    feats = [TP.features_from_fbank(fb[b]) for b in range(n_utt)]
+    if beam_k:
+        port.beam(feats, beam_k)
+    else:
+        port.greedy(feats)
     dt = time.perf_counter() - t0
-    return {"value": n_utt / dt, "unit": "utt/s", "cores": int(cores), "kind": "port",
-            "sample": f"greedy, {n_utt} utterances x T={T} (all 40 steps), numpy fp32 oracle, {dt:.2f} s"}
+    mode = f"beam {beam_k}" if beam_k else "greedy"
+    rec = {"value": n_utt / dt, "unit": "utt/s", "cores": int(cores), "kind": "port",
+           "sample": f"{mode}, {n_utt} utterances x T={T} in one batch (all 40 steps), torch-CPU port "
+                     f"(oracle/torch_port.py) on {cores} threads, {dt:.2f} s"}
+    try:  # the port's speed relative to the reference's own CPU path, measured in the container
+        cal = json.load(open(CPU_CALIBRATION))
+        key = "beam8" if beam_k else "greedy"
+        rec["ref_ratio"] = cal[key]["port_over_reference"]
+        rec["ref_ratio_note"] = cal[key]["note"]
+        rec["reference_equiv_value"] = rec["value"] / rec["ref_ratio"]
+    except Exception:
+        pass
+    return rec
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def relaunch(n):
+    """Run this script under torch.distributed.run with n ranks (one per GPU) and return its exit
+    status.  Called before anything touches the GPU; device_count() does not initialise it."""
+    import torch
+    have = torch.cuda.device_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -127,21 +181,29 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--frames", type=int, default=800)
     ap.add_argument("--beam", type=int, default=8)
-    ap.add_argument("--beam-batch", type=int, default=128)
-    ap.add_argument("--beam-steps", type=int, default=2)
+    ap.add_argument("--beam-batch", type=int, default=256,
+                    help="per-GPU batch of the metric's beam line (BASELINE.json: B = 256, beam 8)")
+    ap.add_argument("--config3-batch", type=int, default=128, help="BASELINE config 3: beam 8 at B = 128")
+    ap.add_argument("--beam-steps", type=int, default=10)
     ap.add_argument("--no-beam", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the BASELINE config 1 (one WAV via main.parse), config 2 (B=32 greedy) and "
                          "config 5 (beam 16 + LM) side lines")
-    ap.add_argument("--cpu-sample", type=int, default=640)
+    ap.add_argument("--cpu-sample", type=int, default=512)
+    ap.add_argument("--cpu-beam-sample", type=int, default=64)
     ap.add_argument("--precision", default="s16x3", choices=["s16x3", "f32"],
                     help="MFMA arithmetic of the timed path (casr_set_precision)")
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the side measurement of the exact-f32 MFMA path")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -200,7 +262,9 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    def timed(fn, steps):
+    flags = {}  # device guard bits read after every timed region (read and clear: all its steps)
+
+    def timed(fn, steps, tag, e=None):
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -211,66 +275,98 @@ def main():
         dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         if dist is not None:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        flags[tag] = (e or eng).device_flags()
         return float(dt.item())
 
+    CLASSES = ["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"]
     for _ in range(args.warmup):
         step_greedy()
-    flags = eng.device_flags()  # decode guard bits: 0 = every index stayed in range
+    flags["warmup"] = eng.device_flags()
     # one instrumented step: per-class launch times -> dominant kernel
-    eng.profile(["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"])
+    eng.profile(CLASSES)
     step_greedy()
     breakdown = eng.profile_read()
     dominant = max(breakdown, key=lambda c: breakdown[c][1])
     # timed region: only the dominant class keeps its event pair per launch
     eng.profile([dominant])
-    dt = timed(step_greedy, args.steps)
+    dt = timed(step_greedy, args.steps, "greedy")
     dom_launches, dom_ms = eng.profile_read()[dominant]
     eng.profile([])
 
     Tp = T // 3
     value = B * world * args.steps / dt
     ms_step = 1000.0 * dt / args.steps
-    work, bound = kernel_work(dominant, B, Tp, B, cfg.vocab, T)
-    per_launch_work = work * args.steps / dom_launches
-    avg_launch_s = dom_ms / 1000.0 / dom_launches
-    if bound == "mfma":
-        peak = PEAK_S16X3_TFLOPS if precision == "s16x3" else PEAK_FP32_TFLOPS
-        achieved, unit = per_launch_work / avg_launch_s / 1e12, "TFLOP/s"
-    else:
-        achieved, peak, unit = per_launch_work / avg_launch_s / 1e9, PEAK_HBM_GBS, "GB/s"
-    # HBM/fabric bytes per launch of the dominant kernel from the committed PMC passes
-    # (tools/probes/pmc_passes.sh -> tools/pmc_summary.py --json: 2 x FETCH_SIZE + WRITE_SIZE)
-    traffic = None
+    pmc = {}
     pmc_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_file):
         try:
-            rec = json.load(open(pmc_file)).get(dominant)
-            traffic = float(rec["hbm_bytes"]) if rec else None
+            pmc = json.load(open(pmc_file))
         except Exception:
-            traffic = None
+            pmc = {}
 
-    beam = None
-    if not args.no_beam:
-        Bb = args.beam_batch
+    def roof(cls, launches, ms, steps, Bc, Rc):
+        """Achieved rate of one kernel class: algorithmic work of `steps` steps over its launches'
+        summed duration, against the peak of its bound; PMC columns from the committed passes."""
+        work, bound = kernel_work(cls, Bc, Tp, Rc, cfg.vocab, T)
+        if not work or not launches or ms <= 0:
+            return None
+        per_launch = work * steps / launches
+        avg_s = ms / 1000.0 / launches
+        if bound == "mfma":
+            peak = PEAK_S16X3_TFLOPS if precision == "s16x3" else PEAK_FP32_TFLOPS
+            ach, unit = per_launch / avg_s / 1e12, "TFLOP/s"
+        else:
+            ach, peak, unit = per_launch / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
+        out = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "frac": ach / peak,
+               "launches": launches, "avg_launch_us": 1e6 * avg_s}
+        rec_p = pmc.get(cls) or {}
+        if rec_p.get("hbm_bytes"):
+            out["traffic"] = float(rec_p["hbm_bytes"])
+            alg = kernel_bytes(cls, Bc, Tp, Rc, cfg.vocab)
+            if alg:
+                out["traffic_over_algorithmic"] = out["traffic"] / alg
+        if rec_p.get("mfma_busy") is not None:
+            out["mfma_busy"] = rec_p["mfma_busy"]
+        return out
+
+    dom = roof(dominant, dom_launches, dom_ms, args.steps, B, B)
+    # every class of the instrumented step (one step: launches and ms of that step)
+    kernels = {c: roof(c, n, ms, 1, B, B) for c, (n, ms) in breakdown.items()}
+    achieved, peak, unit, bound = dom["achieved"], dom["peak"], dom["unit"], dom["bound"]
+    avg_launch_s = dom["avg_launch_us"] / 1e6
+    traffic = dom.get("traffic")
+
+    def beam_line(Bb, k, steps, tag):
         fbb = torch.from_numpy(fbank_batch(rank * Bb, Bb, T)).to(dev)
         frb = torch.full((Bb,), T, dtype=torch.int32, device=dev)
 
         def step_beam():
             eng.encode_fbank(fbb, frb)
-            r = eng.beam(args.beam)
-            return to_host(r["tokens"], "beam")
+            r = eng.beam(k)
+            return to_host(r["tokens"], tag)
 
         step_beam()
-        dtb = timed(step_beam, args.beam_steps)
+        flags[tag + "_warmup"] = eng.device_flags()
+        dtb = timed(step_beam, steps, tag)
         # one instrumented beam step after the timed region: per-class milliseconds
-        eng.profile(["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"])
+        eng.profile(CLASSES)
         step_beam()
-        beam_breakdown = {c: round(v[1], 3) for c, v in eng.profile_read().items()}
+        bd = eng.profile_read()
         eng.profile([])
-        beam = {"k": args.beam, "batch_per_gpu": Bb, "value": Bb * world * args.beam_steps / dtb,
-                "unit": "utt/s", "ms_per_step": 1000.0 * dtb / args.beam_steps,
-                "rtf": dtb / args.beam_steps / (Bb * world * AUDIO_S_PER_UTT),
-                "kernel_breakdown_ms": beam_breakdown}
+        return {"k": k, "batch_per_gpu": Bb, "value": Bb * world * steps / dtb, "steps": steps,
+                "unit": "utt/s", "ms_per_step": 1000.0 * dtb / steps,
+                "rtf": dtb / steps / (Bb * world * AUDIO_S_PER_UTT),
+                "kernel_breakdown_ms": {c: round(v[1], 3) for c, v in bd.items()},
+                "kernels": {c: roof(c, n, ms, 1, Bb, Bb * k) for c, (n, ms) in bd.items()}}
+
+    beam = config3 = None
+    if not args.no_beam:
+        # the metric's beam line: beam 8 at B = 256 per GPU (R = 2048 decode rows)
+        beam = beam_line(args.beam_batch, args.beam, args.beam_steps, "beam")
+        # BASELINE config 3: beam 8 at B = 128 per GPU (config 4 at --gpus 8: 1024 utterances)
+        if not args.no_configs:
+            config3 = beam_line(args.config3_batch, args.beam, args.beam_steps, "config3")
+            config3["config"] = "BASELINE config 3 (config 4 at --gpus 8): beam 8, B=128/GPU, T=800"
 
     # BASELINE config 2: a B = 32 greedy batch (same weights, same step)
     small = None
@@ -284,7 +380,7 @@ def main():
             return to_host(eng.greedy()["tokens"], "small")
 
         step_small()
-        dts = timed(step_small, args.steps)
+        dts = timed(step_small, args.steps, "config2")
         small = {"config": "BASELINE config 2: greedy, B=32/GPU, T=800", "batch_per_gpu": Bs,
                  "value": Bs * world * args.steps / dts, "unit": "utt/s", "ms_per_step": 1000.0 * dts / args.steps}
 
@@ -321,7 +417,7 @@ def main():
     lm_line = None
     if not args.no_configs:
         from casr.results import records_by_utterance, second_pass_select
-        Bl, kl = args.beam_batch, 16
+        Bl, kl = args.config3_batch, 16
         eng5 = Engine(cfg, *synthetic_state_dicts(cfg, peaked=True), device=dev)
         eng5.set_precision(args.precision)
         fbl = torch.from_numpy(fbank_batch(rank * Bl, Bl, T)).to(dev)
@@ -375,7 +471,7 @@ def main():
         # adds ~50 ms to the batch it lands in (measured, tools/probes/config5_probe.py)
         gc.collect()
         gc.freeze()
-        dtl = timed(lambda: run_lm(args.beam_steps), 1)
+        dtl = timed(lambda: run_lm(args.beam_steps), 1, "config5", e=eng5)
         gc.unfreeze()
         lm_line = {"config": "BASELINE config 5: beam 16 + second-pass LM rescoring (stub LM, host)",
                    "k": kl, "batch_per_gpu": Bl, "value": Bl * world * args.beam_steps / dtl, "unit": "utt/s",
@@ -391,7 +487,7 @@ def main():
     if precision == "s16x3" and not args.no_f32_compare:
         eng.set_precision("f32")
         step_greedy()
-        dtf = timed(step_greedy, max(2, args.steps // 2))
+        dtf = timed(step_greedy, max(2, args.steps // 2), "f32")
         nf = max(2, args.steps // 2)
         f32_cmp = {"value": B * world * nf / dtf, "unit": "utt/s", "ms_per_step": 1000.0 * dtf / nf}
         eng.set_precision(precision)
@@ -399,6 +495,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_sample, T)
+        if beam is not None and args.cpu_beam_sample > 0:
+            beam["cpu_baseline"] = cpu_baseline(args.cpu_beam_sample, T, beam_k=args.beam)
+            beam["speedup_vs_cpu"] = beam["value"] / beam["cpu_baseline"]["value"]
 
     if rank == 0:
         rec = {
@@ -416,6 +515,7 @@ def main():
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
             "rtf": dt / args.steps / (B * world * AUDIO_S_PER_UTT),
             "beam": beam,
+            "config3_beam8_b128": config3,
             "roofline": {"kernel": dominant, "bound": bound, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": achieved / peak, "traffic": traffic,
                          "traffic_unit": "bytes per launch (PMC 2 x FETCH_SIZE + WRITE_SIZE)",
@@ -427,7 +527,11 @@ def main():
                          **({"latency_bound": True, "per_step_us": 1e6 * avg_launch_s / Tp,
                              "note": "serial chain of Tp dependent steps per layer; per-step time is "
                                      "hand-off latency + MFMA + cell (DESIGN.md 3.2)"}
-                            if dominant == "rec_step" else {})},
+                            if dominant == "rec_step" else {}),
+                         "kernels": kernels,
+                         "kernels_note": "every kernel class of one instrumented greedy step (HIP events): "
+                                         "achieved = algorithmic work / launch time; traffic / mfma_busy from "
+                                         "the committed PMC passes (profiles/pmc_traffic.json)"},
             "config2_greedy_b32": small,
             "config1_single_wav": single,
             "config5_beam16_lm": lm_line,
@@ -435,6 +539,7 @@ def main():
             "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},
             "weights_bcast_s": weight_s,
             "device_flags": flags,
+            "device_flags_clean": all(v == 0 for v in flags.values()),
             "cpu_baseline": cpu,
         }
         if cpu:

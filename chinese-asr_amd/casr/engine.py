@@ -5,6 +5,7 @@ compute step is a call into the HIP C-ABI library.  There is no CPU or torch-op 
 without a GPU or the library, construction raises.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -45,6 +46,11 @@ class Engine:
             self.bind(packed)
         self._B = self._Tp = None
         self.requested = "s16x3"
+        # A/B tooling hook (tools/probes): CASR_OPTS="REC_SLEEP=2,REC_POLL_GAP=3" sets tuning
+        # options on every new handle; the library itself reads no environment
+        for item in filter(None, os.environ.get("CASR_OPTS", "").split(",")):
+            name, val = item.split("=")
+            self.set_option(name.strip(), int(val))
 
     def bind(self, packed):
         """packed: host numpy blob or a device tensor (e.g. received by RCCL broadcast)."""
@@ -178,7 +184,8 @@ class Engine:
         return rt, rs, rv
 
     def device_flags(self):
-        """Guard bits of the last decode (0 = clean); synchronises the stream."""
+        """Guard bits raised since the previous read (read and clear: every encode / decode in
+        between is covered; 0 = clean); synchronises the stream."""
         f = ctypes.c_int32()
         _lib.check(self.lib.casr_device_flags(self.handle, ctypes.byref(f), _stream()), self.handle)
         return f.value
@@ -223,6 +230,15 @@ class Engine:
             finally:
                 self.set_precision(req)
         return out, f
+
+    def set_option(self, name, value):
+        """Tuning option (include/casr.h CASR_OPT_*, lib.OPTIONS): speed only, same bits."""
+        _lib.check(self.lib.casr_set_option(self.handle, _lib.OPTIONS[name], int(value)), self.handle)
+
+    def get_option(self, name):
+        v = ctypes.c_int32()
+        _lib.check(self.lib.casr_get_option(self.handle, _lib.OPTIONS[name], ctypes.byref(v)), self.handle)
+        return v.value
 
     def precision(self):
         """Effective arithmetic of the MFMA contractions ('s16x3' or 'f32')."""

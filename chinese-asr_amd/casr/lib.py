@@ -22,10 +22,15 @@ EXPORTS = [
     "casr_beam_records", "casr_profile_enable", "casr_profile_read", "casr_set_graphs",
     "casr_device_flags", "casr_set_persistent", "casr_recurrence_mode", "casr_log_mel",
     "casr_log_mel_frames", "casr_mel_filterbank", "casr_set_precision", "casr_get_precision",
+    "casr_set_option", "casr_get_option",
 ]
 
 # arithmetic of the MFMA contractions (casr_set_precision)
 PRECISIONS = {"f32": 0, "s16x3": 1}
+
+# tuning options (include/casr.h CASR_OPT_*): speed only, every value gives the same bits
+OPTIONS = {"FUSE_SELECT": 0, "REC_LAYOUT": 1, "REC_STORE_PLAIN": 2, "REC_SLEEP": 3, "REC_POLL_GAP": 4,
+           "REC_COOP": 5, "GEMM16_PERSIST": 6, "GEMM16_TAIL": 7, "ATTN_KPB": 8}
 
 # kernel classes of casr_profile_enable / casr_profile_read (include/casr.h)
 KERNEL_CLASSES = ["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"]
@@ -100,12 +105,14 @@ def load(path=None):
         "casr_log_mel_frames": (i32, [i32]),
         "casr_mel_filterbank": (i32, [i32, f32, f32, i32, vp]),
         "casr_profile_read": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)]),
+        "casr_set_option": (i32, [vp, i32, i32]),
+        "casr_get_option": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.casr_api_version() != 2:
+    if lib.casr_api_version() != 3:
         raise CasrError("casr library API version mismatch")
     _LIB = lib
     return lib

@@ -123,7 +123,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
   const int apg = (A + G - 1) / G;
   const float* kb = keysT + (size_t)b * A * Tq;
-  constexpr int CH = AT_CH;
+  constexpr int CH = KPB >= 8 ? AT_CH / 2 : AT_CH;  // KPB 8: half the keys rows per batch (registers)
   // this thread's score work: (a-group, 4-step chunk) items it = tid, tid + 512, ...; each in
   // batches of CH keys rows
   auto score_item = [&](int it, bool first, auto&& after_loads) {
@@ -291,9 +291,12 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     // (alpha is finite everywhere: 0 past len) and the loop needs no exit test per t
     auto alpha = [&](int t, float (&al)[KPB]) {
       const float* ep = es + min(t, Tq - 1) * KPB;
-      if constexpr (KPB == 4) {
-        const float4 a4 = *reinterpret_cast<const float4*>(ep);
-        al[0] = a4.x, al[1] = a4.y, al[2] = a4.z, al[3] = a4.w;
+      if constexpr (KPB % 4 == 0) {
+#pragma unroll
+        for (int q = 0; q < KPB / 4; ++q) {
+          const float4 a4 = *reinterpret_cast<const float4*>(ep + 4 * q);
+          al[4 * q] = a4.x, al[4 * q + 1] = a4.y, al[4 * q + 2] = a4.z, al[4 * q + 3] = a4.w;
+        }
       } else {
 #pragma unroll
         for (int j = 0; j < KPB; ++j) al[j] = ep[j];
@@ -315,7 +318,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       alpha(t, al);
       fma4(al, v);
     }
-    constexpr int CT = 32;
+    constexpr int CT = KPB >= 8 ? 16 : 32;  // value rows in flight per lane (KPB 8: fewer, the accumulators double)
     for (int tb = t; tb < len; tb += 4 * CT) {
       float4 v4[CT];
 #pragma unroll
@@ -354,17 +357,10 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   stamp(5);
 }
 
-// value rows prefetched into LDS by each block: what fits beside the block's other LDS (160 KiB
-// per CU, one block per CU), a multiple of 4 rows
-// CASR_ATTN_LDS_KB: LDS budget per block in KiB (tuning knob; default 156 = one block per CU)
-static size_t attn_lds_budget() {
-  static const size_t v = [] {
-    const char* e = std::getenv("CASR_ATTN_LDS_KB");
-    const int kb = e ? std::atoi(e) : 156;
-    return (size_t)(kb > 16 && kb <= 156 ? kb : 156) * 1024;
-  }();
-  return v;
-}
+// value rows prefetched into LDS by each block: what fits beside the block's other LDS (156 KiB
+// of the 160 KiB per CU, one block per CU), a multiple of 4 rows.  Round 2 measured a smaller
+// budget (two blocks per CU) unchanged; the knob was removed in round 3.
+static size_t attn_lds_budget() { return (size_t)156 * 1024; }
 
 template <int KPB>
 static int attn_npf(int Tp) {
@@ -393,23 +389,36 @@ static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart,
   return hipGetLastError();
 }
 
-hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
-                                 int32_t* newdone, int l, int total, hipStream_t s) {
-  if (a.k == 1) return launch_kpb<1>(a, st, qpart, align, newdone, l, total, s);
-  if (a.k == 2) return launch_kpb<2>(a, st, qpart, align, newdone, l, total, s);
-  // k > 4 keeps 4 rows per block: 8 rows per block (one block per utterance, half the grid)
-  // measured 3.68 ms vs 2.87 ms per B = 128, k = 8 batch.  CASR_ATTN_KPB = 1 or 2: tuning knob
-  static const int kpb = [] {
-    const char* e = std::getenv("CASR_ATTN_KPB");
-    return e ? std::atoi(e) : 4;
-  }();
-  if (kpb == 1) return launch_kpb<1>(a, st, qpart, align, newdone, l, total, s);
-  if (kpb == 2) return launch_kpb<2>(a, st, qpart, align, newdone, l, total, s);
-  return launch_kpb<4>(a, st, qpart, align, newdone, l, total, s);
+// beam rows per block at k > 2 (CASR_OPT_ATTN_KPB, 0 = auto).  4 rows per block at B < 256: 8 rows
+// per block (one block per utterance, half the grid at B = 128) measured 3.68 ms vs 2.87 ms per
+// B = 128, k = 8 batch, and 2 or 1 rows per block 2.81 / 3.57 ms against 2.80 (round 2).  At B >= 256
+// one block per utterance already covers the CUs and streams each utterance's keys and values once
+// per step instead of k / 4 times (auto: 8 rows per block there).
+int attention_kpb(int B, int k, int opt) {
+  if (k == 1) return 1;
+  if (k == 2) return 2;
+  if (opt == 4 || opt == 8) return opt;
+  return B >= 256 && k >= 8 ? 8 : 4;
 }
 
-size_t attention_smem_bytes(int k, int Tp) {
-  const size_t f = k == 1 ? attn_smem_floats<1>(Tp) : k == 2 ? attn_smem_floats<2>(Tp) : attn_smem_floats<4>(Tp);
+hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
+                                 int32_t* newdone, int l, int total, hipStream_t s) {
+  switch (attention_kpb(a.B, a.k, a.attn_kpb)) {
+    case 1: return launch_kpb<1>(a, st, qpart, align, newdone, l, total, s);
+    case 2: return launch_kpb<2>(a, st, qpart, align, newdone, l, total, s);
+    case 8: return launch_kpb<8>(a, st, qpart, align, newdone, l, total, s);
+    default: return launch_kpb<4>(a, st, qpart, align, newdone, l, total, s);
+  }
+}
+
+size_t attention_smem_bytes(int B, int k, int Tp, int opt) {
+  size_t f;
+  switch (attention_kpb(B, k, opt)) {
+    case 1: f = attn_smem_floats<1>(Tp); break;
+    case 2: f = attn_smem_floats<2>(Tp); break;
+    case 8: f = attn_smem_floats<8>(Tp); break;
+    default: f = attn_smem_floats<4>(Tp); break;
+  }
   return f * sizeof(float);
 }
 

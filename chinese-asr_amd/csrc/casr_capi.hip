@@ -15,7 +15,6 @@
 
 namespace casr {
 
-size_t attention_smem_bytes(int k, int Tp);  // decoder.hip
 
 // version word of the packed layout (bump whenever make_layout or a packer changes)
 constexpr uint32_t LAYOUT_MAGIC = 0xCA5B0003u;
@@ -165,9 +164,11 @@ struct casr_handle {
   DevBuf feat;     // casr_encode_fbank outside the s16x3 image path: the f32 features
   DevBuf fstat;    // feature statistics scratch [B][2][D] (features.hip)
   DevBuf hx;       // persistent recurrence: tagged h words [3][2][Bp][H]
-  DevBuf eflag;    // encoder device guard bits (CASR_DEV_REC_TIMEOUT)
+  // device guard bits, one word per source: [0] decode, [1] encoder + features, [2] front end.
+  // Allocated and zeroed once; kernels OR bits in; casr_device_flags reads and clears them, so
+  // they cover every call since the previous read (never reset inside a captured graph)
+  DevBuf gflags;
   DevBuf fe_const; // FrontendConst (filterbank, window, twiddles), built on first casr_log_mel
-  DevBuf fflag;    // front-end device guard bits (CASR_DEV_BAD_AUDIO)
   bool use_persistent = true;
   int precision = CASR_PREC_S16X3;  // requested (casr_set_precision)
   bool s16_valid = false;           // the bound blob's s16 images are usable (Layout::info)
@@ -189,9 +190,23 @@ struct casr_handle {
   hipStream_t xs[2] = {};         // replay streams, fenced to the caller's stream by events
   hipEvent_t ev_in = nullptr, ev_out[2] = {};
   GraphCache graphs;
+  Tuning tune;  // casr_set_option
 };
 
 static int fail(casr_handle* h, int code, const char* fmt, ...);
+
+// the handle's guard words (allocated and zeroed on first use; the caller has set the device)
+static int32_t* guard_words(casr_handle* h) {
+  if (!h->gflags.p) {
+    if (h->gflags.ensure(64) != hipSuccess) return nullptr;
+    if (hipMemset(h->gflags.p, 0, 64) != hipSuccess) {
+      h->gflags.release();
+      return nullptr;
+    }
+  }
+  return h->gflags.as<int32_t>();
+}
+#define GUARD(h, i) (guard_words(h) + (i))
 
 // Capture `body(stream)` once per key into a hipGraph on the handle's private capture stream,
 // then replay it on the private replay stream, ordered after everything already enqueued on
@@ -449,7 +464,7 @@ void casr_destroy(casr_handle* h) {
     if (h->ev_out[i]) (void)hipEventDestroy(h->ev_out[i]);
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
-  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->eflag, &h->fe_const, &h->fflag,
+  for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->gflags, &h->fe_const,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout})
     b->release();
   delete h;
@@ -469,9 +484,35 @@ int casr_set_persistent(casr_handle* h, int enable) {
 
 int casr_recurrence_mode(const casr_handle* h, int B) {
   if (!h || B <= 0) return -1;
-  // the persistent recurrence needs every workgroup of its grid resident at once
-  if (!h->use_persistent || hipSetDevice(h->device) != hipSuccess) return 0;
-  return rec_layer_fits(B) ? 1 : 0;
+  if (!h->use_persistent) return 0;
+  // the persistent recurrence needs every workgroup of its grid resident at once; the occupancy
+  // query runs on the handle's device, and the caller's current device is restored
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return 0;
+  if (cur != h->device && hipSetDevice(h->device) != hipSuccess) return 0;
+  const int fits = rec_layer_fits(B, rec_layout(B, h->tune)) ? 1 : 0;
+  if (cur != h->device) (void)hipSetDevice(cur);
+  return fits;
+}
+
+int casr_set_option(casr_handle* h, int option, int value) {
+  if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
+  if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8};
+  if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
+    return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
+  if (value < lo[option] || value > hi[option])
+    return fail(h, CASR_ERR_ARG, "option %d: value %d not in [%d, %d]", option, value, lo[option], hi[option]);
+  h->tune.v[option] = value;
+  return CASR_OK;
+}
+
+int casr_get_option(const casr_handle* h, int option, int32_t* value) {
+  if (!h || !value || option < 0 || option >= CASR_OPT_COUNT)
+    return fail(nullptr, CASR_ERR_ARG, "casr_get_option: bad arguments");
+  *value = h->tune[option];
+  return CASR_OK;
 }
 
 const char* casr_last_error(const casr_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
@@ -512,11 +553,10 @@ int casr_log_mel(casr_handle* h, const float* wav, const int32_t* n_samples, int
     HIP_OK(h, h->fe_const.ensure(sizeof(FrontendConst)));
     HIP_OK(h, hipMemcpy(h->fe_const.p, &c, sizeof c, hipMemcpyHostToDevice));
   }
-  HIP_OK(h, h->fflag.ensure(16));
-  HIP_OK(h, hipMemsetAsync(h->fflag.p, 0, 16, s));
+  if (!guard_words(h)) return fail(h, CASR_ERR_HIP, "casr_log_mel: guard words not allocated");
   ProfScope ps(&h->prof, CASR_K_FEATURES, s);
   HIP_OK(h, launch_log_mel(wav, n_samples, B, n_max, t_max, preemphasis, h->fe_const.as<FrontendConst>(), fbank,
-                           frames, h->fflag.as<int32_t>(), s));
+                           frames, GUARD(h, 2), s));
   return CASR_OK;
 }
 
@@ -545,21 +585,22 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
   HIP_OK(h, h->keysT.ensure((size_t)B * A * Tq * sizeof(float)));
   HIP_OK(h, h->lens.ensure((size_t)B * sizeof(int32_t)));
   if (!fb) HIP_OK(h, hipMemcpyAsync(h->lens.p, lens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
-  const bool persistent = casr_recurrence_mode(h, B) == 1;
+  const int layout = rec_layout(B, h->tune);
+  bool persistent = casr_recurrence_mode(h, B) == 1;
   if (!persistent) {  // the persistent recurrence writes the padded frames itself
     HIP_OK(h, hipMemsetAsync(h->out0.p, 0, rows * C * sizeof(float), s));
     HIP_OK(h, hipMemsetAsync(h->out1.p, 0, rows * C * sizeof(float), s));
   }
-  HIP_OK(h, h->eflag.ensure(16));
-  {  // final h and the encoder guard words: one launch
+  if (!guard_words(h)) return fail(h, CASR_ERR_HIP, "casr_encode: guard words not allocated");
+  int32_t* eflag = GUARD(h, 1);
+  {  // final h
     FillList fl;
     fl.add32(h->hfin.p, 0u, (size_t)2 * B * H);
-    fl.add32(h->eflag.p, 0u, 4);
     HIP_OK(h, fill_multi(fl, s));
   }
   const bool s16 = h->s16();
   if (s16) HIP_OK(h, h->x16.ensure(rows * s16_kpad(D) * sizeof(float)));
-  if (persistent) HIP_OK(h, h->hx.ensure(rec_layer_granule_bytes(B)));
+  if (persistent) HIP_OK(h, h->hx.ensure(rec_layer_granule_bytes(B, layout)));
   const int32_t* dl = h->lens.as<int32_t>();
   float* outs[2] = {h->out0.as<float>(), h->out1.as<float>()};
   bool x16_ready = false;
@@ -569,7 +610,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
     if (s16 && features_x16_supported(T)) {
       HIP_OK(h, launch_features_x16(fb, frames, B, T, eps, h->lens.as<int32_t>(), h->fstat.as<float>(),
                                     h->x16.as<uint16_t>(), s16_kpad(D),
-                                    h->eflag.as<int32_t>(), s));
+                                    eflag, s));
       x16_ready = true;  // feat stays NULL: layer 0 reads only the image (no residual input)
     } else {
       HIP_OK(h, h->feat.ensure(rows * D * sizeof(float)));
@@ -579,9 +620,8 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
   }
   const float* x = feat;
   float* hb = h->hbuf.as<float>();
-  // s16: a persistent layer writes the next layer's input row image itself (no split pass);
-  // CASR_FUSE_SPLIT=0 restores the separate split_rows pass (A/B knob)
-  static const bool fuse_split = [] { const char* e = std::getenv("CASR_FUSE_SPLIT"); return !e || std::atoi(e) != 0; }();
+  // s16: a persistent layer writes the next layer's input row image itself (no split pass)
+  bool fell_back = false;  // a cooperative persistent launch was refused: per-step from here on
   for (int l = 0; l < h->cfg.enc_layers; ++l) {
     const int din = l == 0 ? D : C;
     float* out = outs[l & 1];
@@ -590,13 +630,10 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
     if (s16) {
       const int kp = s16_kpad(din);
       if (!x16_ready)
-        HIP_OK(h, launch_split_rows(x, din, (int)rows, din, kp, h->x16.as<uint16_t>(), h->eflag.as<int32_t>(), s));
-      if (gemm16_waves() == 0)
-        HIP_OK(h, launch_input_proj_s16(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
-                                        h->W + h->L.enc_bias[l], h->gin.as<float>(), s));
-      else
-        HIP_OK(h, launch_input_proj_s16_big(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
-                                            h->W + h->L.enc_bias[l], h->gin.as<float>(), s, din));
+        HIP_OK(h, launch_split_rows(x, din, (int)rows, din, kp, h->x16.as<uint16_t>(), eflag, s));
+      HIP_OK(h, launch_input_proj_s16_big(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
+                                          h->W + h->L.enc_bias[l], h->gin.as<float>(), s, din,
+                                          h->tune[CASR_OPT_GEMM16_PERSIST], h->tune[CASR_OPT_GEMM16_TAIL]));
     } else {
       HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
                                   h->gin.as<float>(), s));
@@ -609,41 +646,55 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
     const float* whh = h->W + (s16 ? h->L.enc_whh16[l] : h->L.enc_whh[l]);
     if (persistent) {
       // one launch runs all Tp steps; h and c start at zero inside (util.py:1236-1247)
-      HIP_OK(h, reset_rec_layer(reinterpret_cast<uint32_t*>(h->hx.p), B, s));
+      HIP_OK(h, reset_rec_layer(reinterpret_cast<uint32_t*>(h->hx.p), B, layout, s));
       // diagnostics only: CASR_REC_TRACE=<file> dumps per-wave phase timestamps of layer 0
       const char* trace_path = l == 0 ? std::getenv("CASR_REC_TRACE") : nullptr;
       DevBuf tbuf;
-      const size_t tbytes = (size_t)rec_layer_grid_blocks(B) * rec_layer_waves(B) * Tp * 5 * sizeof(uint32_t);
+      const size_t tbytes = (size_t)rec_layer_grid_blocks(B, layout) * rec_layer_waves(layout) * Tp * 5 * sizeof(uint32_t);
       if (trace_path) {
         HIP_OK(h, tbuf.ensure(tbytes));
         HIP_OK(h, hipMemsetAsync(tbuf.p, 0, tbytes, s));
       }
+      hipError_t er;
       {
         ProfScope ps(&h->prof, CASR_K_REC_STEP, s);
         // the last layer's image feeds the keys GEMM
-        uint16_t* x16o = (s16 && fuse_split) ? h->x16.as<uint16_t>() : nullptr;
-        HIP_OK(h, launch_rec_layer(whh, h->gin.as<float>(), xin, out, x16o,
-                                   reinterpret_cast<uint32_t*>(h->hx.p), h->hfin.as<float>(),
-                                   h->cst.as<float>(), dl, B, Tp, residual, s16, h->eflag.as<int32_t>(),
-                                   tbuf.as<uint32_t>(), s));
+        uint16_t* x16o = s16 ? h->x16.as<uint16_t>() : nullptr;
+        er = launch_rec_layer(whh, h->gin.as<float>(), xin, out, x16o, reinterpret_cast<uint32_t*>(h->hx.p),
+                              h->hfin.as<float>(), h->cst.as<float>(), dl, B, Tp, residual, s16,
+                              eflag, tbuf.as<uint32_t>(), layout, h->tune, s);
       }
-      if (trace_path) {
+      if (er == hipErrorCooperativeLaunchTooLarge) {
+        // the device cannot hold the whole grid at once (e.g. CUs taken by other work): this layer
+        // and the next ones run the per-step recurrence (same bits) instead of spinning
+        (void)hipGetLastError();
+        persistent = false;
+        fell_back = true;
+      } else {
+        HIP_OK(h, er);
+      }
+      if (persistent && trace_path) {
         std::vector<uint32_t> hostv(tbytes / 4);
         HIP_OK(h, hipMemcpyAsync(hostv.data(), tbuf.p, tbytes, hipMemcpyDeviceToHost, s));
         HIP_OK(h, hipStreamSynchronize(s));
         tbuf.release();
         if (FILE* f = std::fopen(trace_path, "wb")) {
-          const int32_t hdr[5] = {rec_layer_grid_blocks(B), rec_layer_waves(B), Tp, 5, rec_layer_producers(B)};
+          const int32_t hdr[5] = {rec_layer_grid_blocks(B, layout), rec_layer_waves(layout), Tp, 5,
+                                  rec_layer_producers(layout)};
           std::fwrite(hdr, sizeof hdr, 1, f);
           std::fwrite(hostv.data(), 4, hostv.size(), f);
           std::fclose(f);
         }
       }
-      x = out;
-      x16_ready = s16 && fuse_split;
-      continue;
+      if (persistent) {
+        x = out;
+        x16_ready = s16;
+        continue;
+      }
     }
     x16_ready = false;
+    // the persistent layers write their padded frames themselves; the per-step ones need zeros
+    if (fell_back) HIP_OK(h, hipMemsetAsync(out, 0, rows * C * sizeof(float), s));
     // h (both ping-pong buffers) and c start at zero (RNN_RES state None, util.py:1236-1247)
     HIP_OK(h, fill_u32(hb, 0, (size_t)2 * 2 * B * H, s));
     HIP_OK(h, fill_u32(h->cst.p, 0, (size_t)2 * B * H, s));
@@ -686,7 +737,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
   // s16x3 keys on every s16 path (the per-step fallback splits the encoder output first), so both
   // recurrences give the same keys bits
   if (s16 && !x16_ready) {
-    HIP_OK(h, launch_split_rows(h->enc_out, C, (int)rows, C, C, h->x16.as<uint16_t>(), h->eflag.as<int32_t>(), s));
+    HIP_OK(h, launch_split_rows(h->enc_out, C, (int)rows, C, C, h->x16.as<uint16_t>(), eflag, s));
     x16_ready = true;
   }
   if (x16_ready)  // s16x3 keys from the image the last persistent layer wrote
@@ -763,7 +814,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   if (k < 1 || k > KMAX_BEAM) return fail(h, CASR_ERR_ARG, "beam width %d not in [1, %d]", k, KMAX_BEAM);
   const int B = h->B, Tp = h->Tp, L = h->cfg.max_len, V = h->cfg.vocab;
   const int R = B * k;
-  const size_t smem = attention_smem_bytes(k, Tp);
+  const size_t smem = attention_smem_bytes(B, k, Tp, h->tune[CASR_OPT_ATTN_KPB]);
   if (smem > 160 * 1024)
     return fail(h, CASR_ERR_UNSUPPORTED, "attention needs %zu B of LDS (k=%d, Tp=%d) > 160 KiB", smem, k, Tp);
   HIP_OK(h, h->st.ensure(((size_t)2 * R * ST + (size_t)(HD / 16) * R * A) * sizeof(float)));
@@ -791,7 +842,8 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   d.newdone = sp + 6 * R;
   d.topfin = reinterpret_cast<uint8_t*>(sp + 6 * R + L);
   d.fin = reinterpret_cast<uint8_t*>(sp + 6 * R + L + B);
-  d.err = sp + 6 * R + L + B + R;
+  if (!guard_words(h)) return fail(h, CASR_ERR_HIP, "decode: guard words not allocated");
+  d.err = GUARD(h, 0);
   d.bp = h->bp.as<int32_t>();
   d.tk = h->tk.as<int32_t>();
   d.rec_score = h->rec.as<float>();
@@ -814,6 +866,8 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   a.temperature = h->cfg.temperature;
   a.s16 = h->s16() ? 1 : 0;
   a.prof = &h->prof;
+  a.fuse_select = h->tune[CASR_OPT_FUSE_SELECT];
+  a.attn_kpb = h->tune[CASR_OPT_ATTN_KPB];
   return CASR_OK;
 }
 
@@ -839,7 +893,7 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   float* ial = align ? iacc + B : nullptr;
   uint8_t* ifin = reinterpret_cast<uint8_t*>(iacc + B + nal);
   a.prof = nullptr;
-  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
+  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
                                      (uint64_t)(align != nullptr), (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->enc_out, (uint64_t)h->keysT.p,
                                      (uint64_t)h->hfin.p, (uint64_t)h->cst.p, (uint64_t)h->lens.p};
@@ -881,7 +935,7 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
   uint32_t lmw, lw;
   std::memcpy(&lmw, &lm_weight, 4);
   std::memcpy(&lw, &length_weight, 4);
-  const std::vector<uint64_t> key = {3, (uint64_t)a.s16, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
+  const std::vector<uint64_t> key = {3, (uint64_t)a.s16, (uint64_t)a.attn_kpb, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
                                      (uint64_t)h->gout.p, (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->bp.p, (uint64_t)h->tk.p, (uint64_t)h->rec.p,
                                      (uint64_t)h->enc_out, (uint64_t)h->keysT.p, (uint64_t)h->hfin.p,
@@ -917,12 +971,13 @@ int casr_device_flags(casr_handle* h, int32_t* flags, void* stream) {
   *flags = 0;
   HIP_OK(h, hipSetDevice(h->device));
   hipStream_t s = (hipStream_t)stream;
-  int32_t dec = 0, enc = 0, fe = 0;
-  if (h->d.err) HIP_OK(h, hipMemcpyAsync(&dec, h->d.err, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  if (h->eflag.p) HIP_OK(h, hipMemcpyAsync(&enc, h->eflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  if (h->fflag.p) HIP_OK(h, hipMemcpyAsync(&fe, h->fflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  HIP_OK(h, hipStreamSynchronize(s));
-  *flags = dec | enc | fe;
+  int32_t w[3] = {0, 0, 0};
+  if (h->gflags.p) {
+    HIP_OK(h, hipMemcpyAsync(w, h->gflags.p, sizeof w, hipMemcpyDeviceToHost, s));
+    HIP_OK(h, hipStreamSynchronize(s));
+    if (w[0] | w[1] | w[2]) HIP_OK(h, hipMemsetAsync(h->gflags.p, 0, sizeof w, s));  // read and clear
+  }
+  *flags = w[0] | w[1] | w[2];
   return CASR_OK;
 }
 

@@ -68,6 +68,12 @@ struct Layout {
 
 Layout make_layout(const casr_config& cfg);
 
+// Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same bits.
+struct Tuning {
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0};
+  int operator[](int i) const { return v[i]; }
+};
+
 // Packed row index of (gate g, unit u) for a gate-interleaved LSTM matrix with hidden
 // size n_hidden: blocks of 16 units, each block = 4 gates x 16 units.
 inline int packed_gate_row(int g, int u) { return (u / 16) * 64 + g * 16 + (u % 16); }
@@ -210,15 +216,11 @@ hipError_t launch_gather_utts(const float* const* ptrs, const int32_t* lens, int
 // encoder.hip
 hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, const float* bias,
                              float* Gin, hipStream_t s);
-// s16x3 input projection: X16 / W16 are s16 row images with Kp (multiple of 32) k per row
-hipError_t launch_input_proj_s16(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                 float* Gin, hipStream_t s);
-// gemm16.hip: the same product on 256 x 256 tiles (Kp % 64 == 0); gemm16_waves() = 0 selects
-// the 128 x 128 kernel instead
-int gemm16_waves();
-// K: the real input width (the images are zero from K to Kp); 0 = Kp
+// gemm16.hip: the s16x3 input projection on 256 x 256 tiles; X16 / W16 are s16 row images with Kp
+// (multiple of 64) k per row.  K: the real input width (the images are zero from K to Kp); 0 = Kp.
+// persist / tail: CASR_OPT_GEMM16_PERSIST / CASR_OPT_GEMM16_TAIL
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                     float* Gin, hipStream_t s, int K = 0);
+                                     float* Gin, hipStream_t s, int K, int persist, int tail);
 hipError_t launch_split_rows(const float* X, int ldx, int M, int K, int Kp, uint16_t* out, int32_t* err,
                              hipStream_t s);
 inline int s16_kpad(int K) { return (K + 63) / 64 * 64; }  // even number of 32-k tiles (gemm16.hip)
@@ -226,18 +228,23 @@ hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xi
                            const float* hprev, float* hnext, float* cst, float* hfin,
                            const int32_t* lens, int B, int Tp, int step, int residual, int row0,
                            int row1, int s16, hipStream_t s);
-// recurrence.hip: persistent per-layer recurrence (all Tp steps in one launch)
-size_t rec_layer_granule_bytes(int B);
-int rec_layer_grid_blocks(int B);
-int rec_layer_waves(int B);  // waves per workgroup (trace layout)
-int rec_layer_producers(int B);  // workgroups per row group (trace layout)
-bool rec_layer_fits(int B);  // the persistent grid for batch B is resident at once (one launch)
-hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s);  // before EVERY launch_rec_layer
+// recurrence.hip: persistent per-layer recurrence (all Tp steps in one launch).  `layout` is the
+// resolved workgroup shape rec_layout(B, opt) returns: 0 = 32 rows x 16 units, 1 = 16 x 32, 2 = 16 x 16
+int rec_layout(int B, const Tuning& t);
+size_t rec_layer_granule_bytes(int B, int layout);
+int rec_layer_grid_blocks(int B, int layout);
+int rec_layer_waves(int layout);      // waves per workgroup (trace layout)
+int rec_layer_producers(int layout);  // workgroups per row group (trace layout)
+bool rec_layer_fits(int B, int layout);  // the persistent grid for batch B is resident at once (one launch)
+hipError_t reset_rec_layer(uint32_t* hx, int B, int layout, hipStream_t s);  // before EVERY launch_rec_layer
 // x16 (s16 only, may be null): also write out's s16 row image [B*Tp][C/32][32 hi | 32 lo] (the
-// next layer's input-GEMM operand, zeros past each length), replacing a split_rows pass
+// next layer's input-GEMM operand, zeros past each length), replacing a split_rows pass.
+// With t[CASR_OPT_REC_COOP] the launch is cooperative: a grid that cannot be co-resident returns
+// an error (hipErrorCooperativeLaunchTooLarge) instead of spinning into the hand-off timeout.
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
-                            int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s);
+                            int residual, int s16, int32_t* err, uint32_t* trace, int layout, const Tuning& t,
+                            hipStream_t s);
 hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc16, const float* b_attn,
                            float* keysT, hipStream_t s);
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
@@ -288,12 +295,15 @@ struct DecodeArgs {
   int s16;               // decoder GEMMs on the s16x3 images (casr_set_precision)
   Profiler* prof;        // may be null
   int greedy_run;        // set by run_greedy: the projection writes per-block argmax partials
+  int fuse_select;       // CASR_OPT_FUSE_SELECT
+  int attn_kpb;          // CASR_OPT_ATTN_KPB (0 auto)
 };
 
 // attention.hip: one decode step's additive attention for all R rows (writes ctx into st)
 hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
                                  int32_t* newdone, int l, int total, hipStream_t s);
-size_t attention_smem_bytes(int k, int Tp);
+size_t attention_smem_bytes(int B, int k, int Tp, int opt);
+int attention_kpb(int B, int k, int opt);  // beam rows per attention block
 void attn_trace_bind(uint32_t* buf);  // CASR_DG_TRACE diagnostics (attention.hip)
 
 void dg_trace_init();  // decoder.hip, CASR_DG_TRACE diagnostics

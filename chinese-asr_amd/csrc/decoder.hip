@@ -1592,7 +1592,6 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
   // fill kernels, not hipMemsetAsync: this sequence is captured into a replayed graph
   FillList fl;
   fl.add32(d.newdone, 0, a.max_len);
-  fl.add32(d.err, 0, 1);
   fl.add8(finished, 0, R);
   fl.add32(out_len, 0, R);
   fl.add32(accum, 0, R);
@@ -1600,13 +1599,9 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
   hipError_t e0 = fill_multi(fl, s);
   if (e0 != hipSuccess) return e0;
   // the select of step l runs inside step l+1's LSTMCell (GreedySel) when the projection writes
-  // per-block partials; the last step's select is a launch of its own.  CASR_FUSE_SELECT=0 keeps
-  // every select a launch (A/B knob, read at every call; the same bits either way)
-  const bool fuse_env = [] {
-    const char* e = std::getenv("CASR_FUSE_SELECT");
-    return !e || std::atoi(e) != 0;
-  }();
-  const bool fuse = fuse_env && row_partials(a);
+  // per-block partials; the last step's select is a launch of its own.  CASR_OPT_FUSE_SELECT = 0
+  // keeps every select a launch (the same bits either way)
+  const bool fuse = a.fuse_select && row_partials(a);
   hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, 1,
                      a.sos, d.tok[0], d.src[0], d.score[0], fuse ? d.src[1] : nullptr);
   for (int l = 0; l < a.max_len; ++l) {
@@ -1644,7 +1639,6 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
   const int R = a.B * a.k;
   FillList fl;
   fl.add32(d.newdone, 0, a.max_len);
-  fl.add32(d.err, 0, 1);
   fl.add8(d.topfin, 0, a.B);
   hipError_t e0 = fill_multi(fl, s);
   if (e0 != hipSuccess) return e0;

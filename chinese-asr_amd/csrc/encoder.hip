@@ -276,17 +276,6 @@ hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, con
   return hipGetLastError();
 }
 
-hipError_t launch_input_proj_s16(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                 float* Gin, hipStream_t s) {
-  const int N = 8 * H;
-  if (Kp % GB_K != 0 || M <= 0) return hipErrorInvalidValue;
-  StoreBiasEpi epi{Gin, bias, N};
-  const TileOrder order = tile_order(N / GB_N, (M + GB_M - 1) / GB_M, Kp);
-  hipLaunchKernelGGL((gemm_nt_kernel<StoreBiasEpi, true>), dim3(order.blocks()), dim3(256), 0, s, X16, Kp, W16,
-                     Kp, M, N, Kp, order, epi);
-  return hipGetLastError();
-}
-
 // f32 rows [M][K] (stride ldx) -> s16 row images [M][Kp/32][32 hi | 32 lo] (zeros past K).
 // One thread per 8 consecutive k: two 16-B stores.  Raises CASR_DEV_F16_RANGE for a finite
 // element beyond the f16 range (its hi would be infinite).

@@ -204,11 +204,9 @@ CASR_DEV void g16_vm_wait() {
 
 // DIAG (tools/probes/gemm16_probe.hip only; results then wrong for 1, 2, 4): 1 = no k-loop DMA
 // (stale LDS), 2 = no MFMA, 4 = no epilogue stores; 8 = iglp_opt(1) in the k loop, 16 = s_setprio 1
-// for waves 4-7 (both measured within noise); 32 = the next stage's DMA issued two instructions
-// at a time between the first k-step's MFMA groups instead of in one burst after the barrier
-// (probe, bitwise equal: Kp 768 628-639 -> 599-618 us, Kp 512 445-467 -> 428-440 us; one per group
-// over both k-steps lands too late, 450-462 us; but inside the encoder, A/B in bench.py, the input
-// projections took 1.96-2.00 ms against 1.93: not launched)
+// for waves 4-7 (both measured within noise).  Round 2 also measured the next stage's DMA issued two
+// instructions at a time between the first k-step's MFMA groups (faster in the probe, equal or
+// slower inside the encoder); removed in round 3.
 template <int DIAG = 0>
 __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __restrict__ A16,
                                                              const float* __restrict__ W16,
@@ -250,12 +248,11 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
   auto stage = [&](int sb, int n, int m, int kt, int tpar) {
     static_for16<0, NQ>([&](auto Q) { stage_slot(sb, n, m, kt, tpar, Q); });
   };
-  constexpr bool IL = (DIAG & 32) != 0;
 
   f32x16 acc[4][NT];
   const _Float16 two11 = (_Float16)2048.0f;
   if ((DIAG & 16) && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  auto compute = [&](const float* src, auto&& issue) {
+  auto compute = [&](const float* src) {
     const float* as = src;
     const float* ws = src + G16_TILE;
     if constexpr ((DIAG & 8) != 0) __builtin_amdgcn_iglp_opt(1);
@@ -280,10 +277,6 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
           acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w1[t], acc[tm][t], 0, 0, 0);
           acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl[t], acc[tm][t], 0, 0, 0);
           acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh[t], acc[tm][t], 0, 0, 0);
-        }
-        if constexpr (IL && ks == 0) {  // NQ = 8 slots over the 4 groups of the first k-step
-          issue(std::integral_constant<int, 2 * tm>{});
-          issue(std::integral_constant<int, 2 * tm + 1>{});
         }
       });
     });
@@ -321,9 +314,8 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
         if (kt + 1 < nk) stage_slot(sb ^ 1, n, m, kt + 1, tpar, Q);
         else if (L2 < total) stage_slot(sb ^ 1, n2, m2, 0, tpar ^ 1, Q);
       };
-      if constexpr (!IL) static_for16<0, NQ>(issue);
-      if (!(DIAG & 2)) compute(lds + sb * G16P_STAGE, issue);
-      else if constexpr (IL) static_for16<0, NQ>(issue);
+      static_for16<0, NQ>(issue);
+      if (!(DIAG & 2)) compute(lds + sb * G16P_STAGE);
       sb ^= 1;
     }
     // epilogue through the stage buffer just consumed (sb ^ 1 now): four rounds of two 32-row
@@ -375,31 +367,8 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
 
 }  // namespace
 
-// CASR_GEMM16_PERSIST: 1 (default) = gemm16_persist_kernel, 0 = gemm16_bias_kernel (A/B knob,
-// read at every launch so a test can compare both); CASR_GEMM16_TAIL=0 keeps the persistent
-// kernel's partial last round instead of the half-tile tail launch
-static bool gemm16_persist() {
-  const char* e = std::getenv("CASR_GEMM16_PERSIST");
-  return !e || std::atoi(e) != 0;
-}
-static bool gemm16_tail() {
-  const char* e = std::getenv("CASR_GEMM16_TAIL");
-  return !e || std::atoi(e) != 0;
-}
-
-// CASR_GEMM16_WAVES: 8 (default) or 4 waves per 256 x 256 tile; 0 = encoder.hip's 128 x 128
-// s16 tile (tuning knob)
-int gemm16_waves() {
-  static const int w = [] {
-    const char* e = std::getenv("CASR_GEMM16_WAVES");
-    const int v = e ? std::atoi(e) : 8;
-    return (v == 0 || v == 4) ? v : 8;
-  }();
-  return w;
-}
-
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                     float* Gin, hipStream_t s, int K) {
+                                     float* Gin, hipStream_t s, int K, int persist, int tail) {
   const int N = 8 * H;
   if (Kp % (2 * G16_K) != 0 || M <= 0 || N % G16_N != 0) return hipErrorInvalidValue;
   const int NB = N / G16_N, NM = (M + G16_M - 1) / G16_M;
@@ -407,7 +376,7 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
   int NG = 1;
   while (NG < 8 && NB % (NG * 2) == 0 && (size_t)(NB / NG) * G16_N * Kp * 4 > (3u << 20)) NG *= 2;
   const Order16 order{NB, NM, NG};
-  if (gemm16_waves() == 8 && gemm16_persist()) {
+  if (persist) {
     static int ncu = [] {
       int dev = 0, v = 0;
       (void)hipGetDevice(&dev);
@@ -425,35 +394,26 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     // wave per SIMD.  Same per-element arithmetic as the persistent kernel: bitwise equal.
     int NMm = NM;
     const int F = NB * NM / ncu;
-    if (gemm16_tail() && F >= 1 && (F * ncu) % NB == 0 && F * ncu / NB < NM) {
+    if (tail && F >= 1 && (F * ncu) % NB == 0 && F * ncu / NB < NM) {
       const int nm = F * ncu / NB;
       const int tail_rows = M - nm * G16_M, NMt = (tail_rows + 127) / 128;
       if (NB * NMt <= ncu) NMm = nm;  // the half tiles fit one round
     }
     const Order16 om{NB, NMm, NG};
     const int total = om.blocks();
-    // CASR_G16_IL=1: the interleaved stage-DMA variant (DIAG 32, A/B knob read at every launch)
-    const char* il = std::getenv("CASR_G16_IL");
-    if (il && std::atoi(il) != 0)
-      hipLaunchKernelGGL(gemm16_persist_kernel<32>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
-                         std::min(M, NMm * G16_M), N, Kp, om, total, nk);
-    else
-      hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
-                         std::min(M, NMm * G16_M), N, Kp, om, total, nk);
+    hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
+                       std::min(M, NMm * G16_M), N, Kp, om, total, nk);
     if (NMm < NM) {
       const size_t r0 = (size_t)NMm * G16_M;
       const int Mt = M - (int)r0, NMt = (Mt + 127) / 128;
-      int NGt = NG;  // XCD grouping of the tail: the same column slices per XCD as the main part
-      const Order16 ot{NB, NMt, NGt};
+      const Order16 ot{NB, NMt, NG};  // XCD grouping of the tail: the same column slices per XCD
       hipLaunchKernelGGL((gemm16_bias_kernel<4, 1>), dim3(ot.blocks()), dim3(256), 0, s, X16 + r0 * Kp, W16, bias,
                          Gin + r0 * N, Mt, N, Kp, ot);
     }
-  } else if (gemm16_waves() == 8)
+  } else {
     hipLaunchKernelGGL(gemm16_bias_kernel<4>, dim3(order.blocks()), dim3(512), 0, s, X16, W16, bias, Gin, M, N, Kp,
                        order);
-  else
-    hipLaunchKernelGGL(gemm16_bias_kernel<2>, dim3(order.blocks()), dim3(256), 0, s, X16, W16, bias, Gin, M, N, Kp,
-                       order);
+  }
   return hipGetLastError();
 }
 

@@ -68,21 +68,6 @@ CASR_DEV void store_granule(uint32_t* p, int step_tagged, float v, int plain) {
     __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_store_dword sc1
 }
 
-// s_waitcnt vmcnt(min(n, 7)) (expcnt / lgkmcnt untouched): the count is an immediate, n is
-// wave-uniform
-CASR_DEV void wait_vm_upto(int n) {
-  switch (n) {
-    case 0: __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8)); break;
-    case 1: __builtin_amdgcn_s_waitcnt(1 | (7 << 4) | (15 << 8)); break;
-    case 2: __builtin_amdgcn_s_waitcnt(2 | (7 << 4) | (15 << 8)); break;
-    case 3: __builtin_amdgcn_s_waitcnt(3 | (7 << 4) | (15 << 8)); break;
-    case 4: __builtin_amdgcn_s_waitcnt(4 | (7 << 4) | (15 << 8)); break;
-    case 5: __builtin_amdgcn_s_waitcnt(5 | (7 << 4) | (15 << 8)); break;
-    case 6: __builtin_amdgcn_s_waitcnt(6 | (7 << 4) | (15 << 8)); break;
-    default: __builtin_amdgcn_s_waitcnt(7 | (7 << 4) | (15 << 8)); break;
-  }
-}
-
 CASR_DEV float decode_granule(uint32_t x) {
   x &= ~TAG_BIT;
   return (x & 0x7FFFFFFFu) == NONFINITE ? __uint_as_float(0x7FC00000u) : __uint_as_float(x);
@@ -101,8 +86,8 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     const float* __restrict__ Whh_f, const float* __restrict__ Gin, const float* __restrict__ xin,
     float* __restrict__ out, uint16_t* __restrict__ x16, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
-    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg, int pre_wait, int pre_sleep,
-    int poll_gap, int store_plain) {
+    int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg, int pre_sleep, int poll_gap,
+    int store_plain) {
   constexpr int NW = RG * UW / 64;      // waves: 4 k-chunks x RG/16 row halves x UW/16 unit halves
   __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
@@ -215,8 +200,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   // for the step's stores).
   // FIRST (step 0, peeled): no sweep, no MFMA.  The later steps have both unconditionally, so every
   // operand load is provably retired by the sweep's vmcnt(0) before its use.
-  int n_after = 0;  // see the end of step()
-  auto step = [&](auto first_c, const int s, const float (&gin_v)[4], const float x_res, float (&gin_n)[4],
+  auto step =[&](auto first_c, const int s, const float (&gin_v)[4], const float x_res, float (&gin_n)[4],
                   float& x_n) -> bool {
     constexpr bool FIRST = decltype(first_c)::value;
     const bool act = s < len;
@@ -232,24 +216,15 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       const __amdgpu_buffer_rsrc_t rs =
           __builtin_amdgcn_make_buffer_rsrc(src, 0, 16 * H * (int)sizeof(uint32_t), 0x00020000);
       const uint32_t want = (s & 1) ? TAG_BIT : 0u;
-      // pacing of the first poll (CASR_REC_PREWAIT / CASR_REC_PRESLEEP, tuning knobs): wait for
-      // this wave's own stores of the previous step (vmcnt(0)), then sleep pre_sleep x 64 clocks.
-      // A poll issued before the group's stores have landed fails and costs a whole extra round
-      // trip.  Measured (ms per greedy batch): no wait 5.95, wait + sleep 0 / 2 / 4 / 5 / 6 / 8 /
-      // 10 = 3.05 / 3.24 / 2.91 / 2.80 / 2.82-2.85 / 2.87 / 2.89; wait + 6.  With the layer
-      // outputs stored after the hand-off word, waiting for the word alone (default 2) measured
-      // 8.29 vs 8.33 ms greedy, 9.33-9.36 vs 9.46 ms beam.  Those numbers predate the plain
-      // hand-off stores and the two-poll passes below, with which the default is no wait.
-      // pre_wait 2: wait for the hand-off word only, not for the vector-memory operations this
-      // wave issued after it (n_after, counted by the previous step from what it actually issued)
-      if (pre_wait == 2) {
-        wait_vm_upto(__builtin_amdgcn_readfirstlane(n_after));
-      } else if (pre_wait) {
-        __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
-      }
+      // pacing of the first poll (CASR_OPT_REC_SLEEP): sleep pre_sleep x 64 clocks.  A poll issued
+      // before the group's stores have landed fails and costs a whole extra round trip.
+      // Measured (round 1, ms per greedy batch, one poll per pass after a wait for the wave's own
+      // stores): no wait 5.95, wait + sleep 0 / 2 / 4 / 5 / 6 / 8 / 10 = 3.05 / 3.24 / 2.91 / 2.80 /
+      // 2.82-2.85 / 2.87 / 2.89.  With the plain hand-off stores and two polls per pass (below) the
+      // own-store wait measured slower (2.67 -> 2.76-2.79 ms) and was removed (round 3).
       for (int i = 0; i < pre_sleep; ++i) __builtin_amdgcn_s_sleep(1);
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      if (poll_gap > 0) {
+      {
         // two polls in flight per pass, the second poll_gap x 64 clocks after the first: a first
         // poll that arrives before the group's last store costs the gap instead of a round trip.
         // Measured on one box, rec ms per greedy batch (3 rounds, interleaved): one poll after
@@ -288,29 +263,6 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
             break;
           }
         }
-      } else
-      for (uint32_t pass = 0;; ++pass) {
-        asm volatile("" ::: "memory");
-        uint32_t bad = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + i * 16, 0, 16 /* sc1 */);
-        // all four loads in flight before any check (hipcc otherwise may interleave load / wait /
-        // check: four round trips per pass)
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) bad |= (v[i].x ^ want) | (v[i].y ^ want) | (v[i].z ^ want) | (v[i].w ^ want);
-        const bool ok = (bad & TAG_BIT) == 0;
-        npass = pass + 1;
-        if (__all(ok)) break;
-        // two independent bounds: wall clock, and a pass count (each pass >= one sc1 round trip)
-        if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS || pass > (1u << 22)) {
-          if (lane == 0) {
-            s_quit[s & 1] = 1;
-            __hip_atomic_fetch_or(err, CASR_DEV_REC_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
       }
       if (tr && lane == 0) tr[s * 5 + 1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
@@ -409,14 +361,6 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       tr[s * 5 + 3] = (uint32_t)__builtin_amdgcn_s_memrealtime();
       tr[s * 5 + 4] = npass;
     }
-    // vector-memory operations issued after the hand-off word, for the next step's pacing wait
-    // (wave-uniform; a store branch no lane of the wave takes issues nothing): the layer output,
-    // hfin on a row's last step, the two image halves, and with the trace the two stamps above plus
-    // the next step's first one.  Only the pacing depends on it: the sweep checks every tag.
-    {
-      const bool any_act = __any(act), any_last = __any(act && s == len - 1);
-      n_after = (any_act ? 1 + (any_last ? 1 : 0) + ((S16 && x16) ? 2 : 0) : 0) + (tr ? 3 : 0);
-    }
     return true;
   };
   float gA[4] = {0.f, 0.f, 0.f, 0.f}, gB[4] = {0.f, 0.f, 0.f, 0.f}, xA = 0.f, xB = 0.f;
@@ -443,26 +387,6 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
 
 }  // namespace
 
-// CASR_REC_LAYOUT = rows x units per workgroup: 32x16 (default), 16x32 or 16x16 (tuning knob)
-static int env_int(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : dflt;
-}
-static int rec_pre_wait() {
-  static const int v = env_int("CASR_REC_PREWAIT", 0);  // 0 none, 1 vmcnt(0), 2 hand-off word only
-  return v;
-}
-static int rec_pre_sleep() {
-  static const int v = env_int("CASR_REC_PRESLEEP", 1);
-  return v;
-}
-// read at every launch (not cached) so a test can compare both hand-off store flavours in one process
-static int rec_store_plain() { return env_int("CASR_REC_STOREPLAIN", 1); }
-static int rec_poll_gap() {
-  static const int v = env_int("CASR_REC_POLLGAP", 2);  // 0: one poll per pass
-  return v;
-}
-
 // CUs of the current device (the persistent grid wants one workgroup per CU)
 static int rec_cus() {
   static const int v = [] {
@@ -480,28 +404,32 @@ static int rec_cus() {
 // a step's MFMA and cell work per CU halves while the hand-off stays a 16-producer exchange.
 // Measured (rec ms per batch, two interleaved rounds): beam B = 128 2.36-2.37 (32x16) -> 2.01-2.02
 // (16x16); greedy B = 256 2.67-2.71 (32x16) vs 3.08-3.10 (16x16: two workgroups per CU).
-// CASR_REC_LAYOUT = 32x16 / 16x32 / 16x16 forces one (tuning knob; read at every call, so a test
-// can run both layouts in one process).
-static int rec_layout(int B) {
-  const char* e = std::getenv("CASR_REC_LAYOUT");
-  if (e) return strcmp(e, "16x32") == 0 ? 1 : strcmp(e, "16x16") == 0 ? 2 : 0;
-  return (H / 16) * ((B + 15) / 16) * 2 <= rec_cus() ? 2 : 0;
+// CASR_OPT_REC_LAYOUT forces one (1 = 32x16, 2 = 16x32, 3 = 16x16).
+int rec_layout(int B, const Tuning& t) {
+  switch (t[CASR_OPT_REC_LAYOUT]) {
+    case 1: return 0;
+    case 2: return 1;
+    case 3: return 2;
+    default: return (H / 16) * ((B + 15) / 16) * 2 <= rec_cus() ? 2 : 0;
+  }
 }
-static int rec_rows(int B) { return rec_layout(B) == 0 ? 32 : 16; }
-static int rec_units(int B) { return rec_layout(B) == 1 ? 32 : 16; }
+static int rec_rows(int layout) { return layout == 0 ? 32 : 16; }
+static int rec_units(int layout) { return layout == 1 ? 32 : 16; }
 
 // the three granule buffers, then the placement table (one word per workgroup)
 static size_t rec_granule_words(int B) { return (size_t)3 * 2 * ((B + 31) / 32 * 32) * H; }
 
-size_t rec_layer_granule_bytes(int B) {
-  return (rec_granule_words(B) + (size_t)rec_layer_grid_blocks(B)) * sizeof(uint32_t);
+size_t rec_layer_granule_bytes(int B, int layout) {
+  return (rec_granule_words(B) + (size_t)rec_layer_grid_blocks(B, layout)) * sizeof(uint32_t);
 }
 
-int rec_layer_waves(int B) { return rec_rows(B) * rec_units(B) / 64; }
+int rec_layer_waves(int layout) { return rec_rows(layout) * rec_units(layout) / 64; }
 
-int rec_layer_producers(int B) { return H / rec_units(B); }
+int rec_layer_producers(int layout) { return H / rec_units(layout); }
 
-int rec_layer_grid_blocks(int B) { return (H / rec_units(B)) * ((B + rec_rows(B) - 1) / rec_rows(B)) * 2; }
+int rec_layer_grid_blocks(int B, int layout) {
+  return (H / rec_units(layout)) * ((B + rec_rows(layout) - 1) / rec_rows(layout)) * 2;
+}
 
 template <int RG, int UW>
 static int occ() {
@@ -516,17 +444,17 @@ static int occ() {
   return v;
 }
 
-bool rec_layer_fits(int B) {
+bool rec_layer_fits(int B, int layout) {
   int per_cu;
-  switch (rec_layout(B)) {
+  switch (layout) {
     case 1: per_cu = occ<16, 32>(); break;
     case 2: per_cu = occ<16, 16>(); break;
     default: per_cu = occ<32, 16>(); break;
   }
-  return rec_layer_grid_blocks(B) <= per_cu * rec_cus();
+  return rec_layer_grid_blocks(B, layout) <= per_cu * rec_cus();
 }
 
-hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
+hipError_t reset_rec_layer(uint32_t* hx, int B, int layout, hipStream_t s) {
   // Guideline 16: re-initialise every call.  Buffer j is first read at step j (j = 1, 2) or 3
   // (j = 0), expecting parity 1, 0, 1: fill buffers 0 and 1 with parity 0, buffer 2 with 1.
   // The placement table after them starts at 0 (no id published).
@@ -534,28 +462,37 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, hipStream_t s) {
   FillList fl;
   fl.add32(hx, 0u, 2 * per);
   fl.add32(hx + 2 * per, TAG_BIT, per);
-  fl.add32(hx + 3 * per, 0u, (size_t)rec_layer_grid_blocks(B));
+  fl.add32(hx + 3 * per, 0u, (size_t)rec_layer_grid_blocks(B, layout));
   return fill_multi(fl, s);
 }
 
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
-                            int residual, int s16, int32_t* err, uint32_t* trace, hipStream_t s) {
-  const int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for every layout
-  const int RG = rec_rows(B), UW = rec_units(B);
-  const int nrg = (B + RG - 1) / RG;
-  dim3 grid((H / UW) * nrg * 2);
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(RG * UW), 0, s, Whh_f, Gin, xin, out, x16, hx, hfin, cst, lens, B, Bp, Tp,
-                       residual, err, trace, nrg, rec_pre_wait(), rec_pre_sleep(), rec_poll_gap(),
-                       rec_store_plain());
+                            int residual, int s16, int32_t* err, uint32_t* trace, int layout, const Tuning& t,
+                            hipStream_t s) {
+  int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for every layout
+  const int RG = rec_rows(layout), UW = rec_units(layout);
+  int nrg = (B + RG - 1) / RG;
+  int sleep = t[CASR_OPT_REC_SLEEP] < 0 ? 0 : t[CASR_OPT_REC_SLEEP] > 16 ? 16 : t[CASR_OPT_REC_SLEEP];
+  int gap = t[CASR_OPT_REC_POLL_GAP] < 1 ? 1 : t[CASR_OPT_REC_POLL_GAP] > 8 ? 8 : t[CASR_OPT_REC_POLL_GAP];
+  int plain = t[CASR_OPT_REC_STORE_PLAIN] ? 1 : 0;
+  const dim3 grid((H / UW) * nrg * 2), block(RG * UW);
+  auto go = [&](auto kern) -> hipError_t {
+    if (t[CASR_OPT_REC_COOP]) {
+      // every workgroup co-resident or an immediate launch error (the hand-off spins need all of them)
+      void* args[] = {&Whh_f, &Gin, &xin, &out, &x16, &hx, &hfin, &cst, &lens, &B, &Bp, &Tp, &residual,
+                      &err, &trace, &nrg, &sleep, &gap, &plain};
+      return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kern), grid, block, args, 0, s);
+    }
+    hipLaunchKernelGGL(kern, grid, block, 0, s, Whh_f, Gin, xin, out, x16, hx, hfin, cst, lens, B, Bp, Tp, residual,
+                       err, trace, nrg, sleep, gap, plain);
+    return hipGetLastError();
   };
-  switch (rec_layout(B)) {
-    case 1: s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>); break;
-    case 2: s16 ? go(rec_layer_kernel<16, 16, true>) : go(rec_layer_kernel<16, 16, false>); break;
-    default: s16 ? go(rec_layer_kernel<32, 16, true>) : go(rec_layer_kernel<32, 16, false>); break;
+  switch (layout) {
+    case 1: return s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>);
+    case 2: return s16 ? go(rec_layer_kernel<16, 16, true>) : go(rec_layer_kernel<16, 16, false>);
+    default: return s16 ? go(rec_layer_kernel<32, 16, true>) : go(rec_layer_kernel<32, 16, false>);
   }
-  return hipGetLastError();
 }
 
 }  // namespace casr

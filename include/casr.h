@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define CASR_API_VERSION 2
+#define CASR_API_VERSION 3
 #define CASR_MAX_LAYERS 8
 
 enum {
@@ -172,8 +172,9 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
 int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uint8_t* rec_valid,
                       void* stream);
 
-/* Guard bits raised by the device since the last casr_encode / casr_greedy / casr_beam
- * (0 = clean): a data-dependent index out of range (1 token, 2 predecessor row, 4 NaN logit
+/* Guard bits raised by the device since the previous casr_device_flags call (read and clear;
+ * they accumulate over every encode / decode / log-mel call in between, so one read after a
+ * series of calls vouches for all of them; 0 = clean): a data-dependent index out of range (1 token, 2 predecessor row, 4 NaN logit
  * row, 8 beam candidate, 16 back-pointer) is clamped and reported here instead of faulting
  * the device; 32 = a bounded hand-off wait of the persistent recurrence expired (results of
  * that casr_encode are invalid); 64 = casr_log_mel got an utterance shorter than 513
@@ -204,8 +205,47 @@ enum { CASR_PREC_F32 = 0, CASR_PREC_S16X3 = 1 };
 int casr_set_precision(casr_handle* h, int precision);
 int casr_get_precision(const casr_handle* h); /* effective mode, -1 on a NULL handle */
 
-/* Which recurrence casr_encode would use for batch B: 1 persistent, 0 per-step, -1 bad args. */
+/* Which recurrence casr_encode would use for batch B: 1 persistent, 0 per-step, -1 bad args.
+ * Does not change the calling thread's current HIP device. */
 int casr_recurrence_mode(const casr_handle* h, int B);
+
+/* Tuning options of one handle.  The defaults are the measured fastest variants;
+ * every value of every option gives the same results bit for bit (tests/test_gpu_parity.py sweeps
+ * them), so an option only ever changes speed.  Options are read at each call and are part of the
+ * keys of the captured hipGraphs, so changing one between calls takes effect at the next call.
+ *   CASR_OPT_FUSE_SELECT     1: greedy select of step l fused into step l+1's LSTMCell (default);
+ *                            0: every select a launch of its own
+ *   CASR_OPT_REC_LAYOUT      persistent recurrence workgroup shape: 0 auto (default: 16 rows x 16
+ *                            units when that grid fits one workgroup per CU, else 32 x 16), 1 32x16,
+ *                            2 16x32, 3 16x16
+ *   CASR_OPT_REC_STORE_PLAIN 1: hand-off words stored L2-kept when the workgroup's whole hand-off
+ *                            group runs on its XCD (checked per launch; default); 0: write-through
+ *   CASR_OPT_REC_SLEEP       pacing of the recurrence's first poll per step, x 64 clocks (default 1)
+ *   CASR_OPT_REC_POLL_GAP    second poll of a pass issued this many x 64 clocks after the first
+ *                            (1..8, default 2)
+ *   CASR_OPT_REC_COOP        1: the persistent recurrence is a cooperative launch, so a grid that
+ *                            cannot be co-resident fails at launch (the encode then falls back to
+ *                            the per-step recurrence) instead of spinning into the hand-off timeout;
+ *                            0: ordinary launch after the occupancy check
+ *   CASR_OPT_GEMM16_PERSIST  1: persistent s16x3 input-projection kernel (default); 0: per tile
+ *   CASR_OPT_GEMM16_TAIL     1: the persistent kernel takes whole rounds of tiles, the rows after
+ *                            them go to one launch of half tiles (default); 0: partial last round
+ *   CASR_OPT_ATTN_KPB        beam rows per attention block at k > 2: 0 auto (8 at B >= 256 and
+ *                            k >= 8, else 4), 4 or 8 */
+enum {
+  CASR_OPT_FUSE_SELECT = 0,
+  CASR_OPT_REC_LAYOUT = 1,
+  CASR_OPT_REC_STORE_PLAIN = 2,
+  CASR_OPT_REC_SLEEP = 3,
+  CASR_OPT_REC_POLL_GAP = 4,
+  CASR_OPT_REC_COOP = 5,
+  CASR_OPT_GEMM16_PERSIST = 6,
+  CASR_OPT_GEMM16_TAIL = 7,
+  CASR_OPT_ATTN_KPB = 8,
+  CASR_OPT_COUNT = 9
+};
+int casr_set_option(casr_handle* h, int option, int value);
+int casr_get_option(const casr_handle* h, int option, int32_t* value_host);
 
 /* The launch-bound loops (each layer's Tp recurrence steps, the whole decode loop) are
  * captured once per shape into hipGraphs on a private stream and replayed on `stream`

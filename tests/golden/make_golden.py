@@ -194,6 +194,16 @@ def decode_suite(name, peaked, frames, out):
     r = m.eval_one_batch_with_beam(dev, 4, feats, lens, None, PUA, second_pass=False,
                                    lm_model=None, lm_weight=1.5, length_weight=1.5)
     meta["beam4_lw"] = rec(r)
+    # softmax temperature (model.py:834 reads gpd['temperature'] at every step; main.py:125 sets
+    # it): round 3 capture, beam 4 and 8 at T = 0.7
+    ref_gpd.gpd["temperature"] = 0.7
+    try:
+        for k in (4, 8):
+            r = m.eval_one_batch_with_beam(dev, k, feats, lens, None, PUA, second_pass=False,
+                                           lm_model=None, lm_weight=0.0, length_weight=0.0)
+            meta[f"beam{k}_t07"] = rec(r)
+    finally:
+        ref_gpd.gpd["temperature"] = 1
     return meta
 
 

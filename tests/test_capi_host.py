@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     assert declared == sorted(L.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.casr_api_version() == 2
+    assert lib.casr_api_version() == 3
 
 
 def test_create_without_gpu_or_bad_config_fails_loudly():
@@ -44,6 +44,15 @@ def test_create_without_gpu_or_bad_config_fails_loudly():
         assert lib.casr_last_error(None)
     with pytest.raises(L.CasrError):
         L.check(3)
+    # tuning options need a handle: a NULL one is refused, not dereferenced
+    v = ctypes.c_int32(-7)
+    assert lib.casr_get_option(None, 0, ctypes.byref(v)) == 1 and v.value == -7
+    assert lib.casr_set_option(None, 0, 1) == 1
+    # the option table of include/casr.h and the binding agree
+    hdr = open(os.path.join(REPO, "include", "casr.h")).read()
+    opts = dict((m.group(1), int(m.group(2))) for m in re.finditer(r"CASR_OPT_([A-Z0-9_]+) = (\d+)", hdr))
+    assert opts.pop("COUNT") == len(L.OPTIONS)
+    assert opts == L.OPTIONS
 
 
 def _layout(cfg):

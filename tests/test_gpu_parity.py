@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import load_golden, fbank_for, golden_frames, near_tie_beam_check
+from golden_util import load_golden, fbank_for, golden_frames, near_tie_beam_check, teacher_forced_score
 from oracle import casr_oracle as O
 from stub_lm import StubLM, pua_int2word
 from casr.config import CasrConfig
@@ -135,8 +135,12 @@ def test_beam_matches_reference(eng, name, k):
     blen = r["length"].cpu().numpy()
     gold = META[name][f"beam{k}"]
     if name == "plain" and k == 16:  # near-tied f32 candidates: test_oracle_golden.py, same check
+        _, dec_sd = synthetic_state_dicts(CFG, peaked=False)
+        enc_sd = synthetic_state_dicts(CFG, peaked=False)[0]
+        feats = [O.features_from_fbank(fbank_for(b, t)) for b, t in enumerate(FRAMES)]
         near_tie_beam_check([toks[b, :blen[b]].tolist() for b in range(len(FRAMES))],
-                            r["score"].cpu().numpy(), gold, atol=2e-3)
+                            r["score"].cpu().numpy(), gold, atol=2e-3,
+                            rescore=lambda b, t: teacher_forced_score(feats[b], t, enc_sd, dec_sd))
         return
     assert [toks[b, :blen[b]].tolist() for b in range(len(FRAMES))] == gold["tokens"]
     np.testing.assert_allclose(r["score"].cpu().numpy(), gold["score"], atol=2e-3, rtol=0)
@@ -219,12 +223,15 @@ def test_graph_replay_equals_eager(eng):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("graphs", [False, True])
 @pytest.mark.parametrize("eos_bias", [0.0, 12.0])
-def test_fused_select_equals_select_launches(eng, eos_bias):
+def test_fused_select_equals_select_launches(eng, eos_bias, graphs):
     """Greedy decoding with each step's select fused into the next LSTMCell (default) and with
-    every select a launch of its own (CASR_FUSE_SELECT=0) give the same tokens, lengths, scores
-    and finished flags bit for bit: ragged lengths, B = 200 (a partial row block), without and
-    with early finishers (eos_bias: rows end at different steps, the early exit counts them)."""
+    every select a launch of its own (CASR_OPT_FUSE_SELECT = 0) give the same tokens, lengths,
+    scores and finished flags bit for bit: ragged lengths, B = 200 (a partial row block), without
+    and with early finishers (eos_bias: rows end at different steps, the early exit counts them).
+    With graphs on, the option is part of the captured graph's key: switching it between calls
+    must replay the other variant, not the first one captured."""
     enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True, eos_bias=eos_bias)
     eng.bind(pack_weights(CFG, enc_sd, dec_sd))
     B = 200
@@ -238,30 +245,36 @@ def test_fused_select_equals_select_launches(eng, eos_bias):
     eng.encode(feat, flen)
     outs = []
     try:
-        eng.set_graphs(False)
-        for fuse in ("0", "1"):
-            os.environ["CASR_FUSE_SELECT"] = fuse
+        eng.set_graphs(graphs)
+        for fuse in (0, 1, 0):
+            eng.set_option("FUSE_SELECT", fuse)
+            if not graphs:  # select launches: one per step, or only the last step's when fused
+                eng.profile(["select"])
             g = eng.greedy()
             assert eng.device_flags() == 0
             outs.append({k: v.cpu() for k, v in g.items() if torch.is_tensor(v)})
+            if not graphs:
+                assert eng.profile_read()["select"][0] == (1 if fuse else CFG.max_len)
+                eng.profile([])
     finally:
-        os.environ.pop("CASR_FUSE_SELECT", None)
+        eng.set_option("FUSE_SELECT", 1)
         eng.set_graphs(True)
     assert outs[0].keys() == outs[1].keys() and "tokens" in outs[0]
-    for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), k
+    for o in outs[1:]:
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], o[k]), k
     if eos_bias:
         assert bool(outs[1]["finished"].any()), "with the EOS bias some rows must finish early"
 
 
-@pytest.mark.parametrize("B,layout", [(37, None), (37, "32x16"), (256, None)])
-def test_persistent_recurrence_equals_per_step(eng, B, layout, monkeypatch):
-    """The persistent per-layer recurrence (granule hand-offs, either store flavour) and the
-    per-step launches give bitwise-identical encoder outputs and final states, on ragged lengths (B = 37: a partial
-    row group and padding rows, in the 16x16 layout the batch selects and in the forced 32x16 one;
-    B = 256: the full 256-workgroup grid of 32x16)."""
-    if layout:
-        monkeypatch.setenv("CASR_REC_LAYOUT", layout)
+@pytest.mark.parametrize("B,layout", [(37, 0), (37, 1), (37, 2), (256, 0)])
+def test_persistent_recurrence_equals_per_step(eng, B, layout):
+    """The persistent per-layer recurrence (granule hand-offs, either store flavour, ordinary or
+    cooperative launch) and the per-step launches give bitwise-identical encoder outputs and
+    final states, on ragged lengths (B = 37: a partial row group and padding rows, in the 16x16
+    layout the batch selects and in the forced 32x16 and 16x32 ones; B = 256: the full
+    256-workgroup grid of 32x16)."""
+    eng.set_option("REC_LAYOUT", layout)
     enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
     eng.bind(pack_weights(CFG, enc_sd, dec_sd))
     rs = np.random.RandomState(11)
@@ -274,20 +287,45 @@ def test_persistent_recurrence_equals_per_step(eng, B, layout, monkeypatch):
                               torch.from_numpy(frames.astype(np.int32)).to(eng.device))
     assert eng.recurrence_mode(B) == 1, "B <= 256 must take the persistent path on MI355X"
     outs = []
-    # the persistent path twice: hand-off words stored plain (L2-kept, the default when each
-    # group shares an XCD) and write-through (CASR_REC_STOREPLAIN=0, read at every launch)
+    # the persistent path three times: hand-off words stored plain (L2-kept, the default when each
+    # group shares an XCD) and write-through (CASR_OPT_REC_STORE_PLAIN = 0), cooperative launch
+    # (default) and ordinary launch (CASR_OPT_REC_COOP = 0)
     try:
-        for persistent, plain in ((False, "1"), (True, "1"), (True, "0")):
-            os.environ["CASR_REC_STOREPLAIN"] = plain
+        for persistent, plain, coop in ((False, 1, 1), (True, 1, 1), (True, 0, 1), (True, 1, 0)):
+            eng.set_option("REC_STORE_PLAIN", plain)
+            eng.set_option("REC_COOP", coop)
             eng.set_persistent(persistent)
             eng.encode(feat, flen)
             assert eng.device_flags() == 0
             outs.append([t.cpu() for t in eng.encoder_results()])
     finally:
-        os.environ.pop("CASR_REC_STOREPLAIN", None)
+        for k, v in (("REC_STORE_PLAIN", 1), ("REC_COOP", 1), ("REC_LAYOUT", 0)):
+            eng.set_option(k, v)
         eng.set_persistent(True)
-    for ref, got in ((outs[0], outs[1]), (outs[1], outs[2])):
-        for a, b in zip(ref, got):
+    for got in outs[1:]:
+        for a, b in zip(outs[0], got):
+            assert torch.equal(a, b)
+
+
+def test_recurrence_pacing_options_bitwise(eng):
+    """The recurrence's pacing options (first-poll sleep, second-poll gap) change only when a
+    workgroup looks at its producers' words, never what it computes: encoder results bitwise equal
+    over the extremes of both (B = 256, T' = 266)."""
+    bind(eng, "peaked")
+    feat, flen = _bench_batch(eng, 256)
+    outs = []
+    try:
+        for sleep, gap in ((1, 2), (0, 1), (16, 8), (4, 1)):
+            eng.set_option("REC_SLEEP", sleep)
+            eng.set_option("REC_POLL_GAP", gap)
+            eng.encode(feat, flen)
+            assert eng.device_flags() == 0
+            outs.append([t.cpu() for t in eng.encoder_results()])
+    finally:
+        eng.set_option("REC_SLEEP", 1)
+        eng.set_option("REC_POLL_GAP", 2)
+    for got in outs[1:]:
+        for a, b in zip(outs[0], got):
             assert torch.equal(a, b)
 
 
@@ -344,22 +382,6 @@ def test_encode_fbank_equals_features_then_encode(eng):
     assert torch.equal(ga, gb)
 
 
-def test_full_length_greedy_matches_oracle(eng):
-    """T = 800 (T' = 266), bench weights (no EOS: all 40 steps), B = 24 vs the CPU oracle."""
-    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True, eos_bias=0.0)
-    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
-    B = 24
-    feat, flen = _bench_batch(eng, B)
-    eng.encode(feat, flen)
-    out = eng.greedy()
-    assert eng.device_flags() == 0
-    toks = out["tokens"].cpu().numpy()
-    feats = [O.features_from_fbank(fbank_for(b, 800)) for b in range(B)]
-    r = O.greedy_decode(feats, [266] * B, enc_sd, dec_sd)
-    np.testing.assert_array_equal(toks, r["all_tokens"])
-    np.testing.assert_allclose(out["accum"].cpu().numpy(), r["accum"], rtol=1e-5, atol=2e-3)
-
-
 def test_batch_invariance_and_determinism(eng):
     """Size-independent properties at the benchmark size B = 256: two runs are bitwise equal,
     and a 16-utterance sub-batch decodes to the same tokens as inside the full batch
@@ -381,8 +403,9 @@ def test_batch_invariance_and_determinism(eng):
     eng.encode(feat[:16].contiguous(), flen[:16].contiguous())
     t2 = eng.beam(8)["tokens"].cpu()
     assert torch.equal(t1[:16], t2)
-    # k = 16: 64 x 16 = 1024 rows (32 projection column blocks: the top-2k threshold comes from the
-    # rows' lane top-2s) against 8 x 16 = 128 rows (64 blocks: from the block partials)
+    # k = 16: 64 x 16 = 1024 rows (the 128 x 160 projection blocks) against 8 x 16 = 128 rows (the
+    # 64 x 80 ones); both take the tile-maxima threshold at temperature 1 (the lanes' top-2 bound
+    # is covered by test_beam_select_threshold_paths_bitwise)
     eng.encode(feat[:64].contiguous(), flen[:64].contiguous())
     t3 = eng.beam(16)["tokens"].cpu()
     assert eng.device_flags() == 0
@@ -476,11 +499,11 @@ def test_model_reruns_f32_on_f16_range_overflow():
 
 
 @pytest.mark.parametrize("B", [256, 128, 37])
-def test_input_gemm_tail_split_bitwise(eng, B, monkeypatch):
+def test_input_gemm_tail_split_bitwise(eng, B):
     """s16x3 input projection: the persistent kernel over whole rounds plus the 128 x 256 half-tile
-    launch for the rows after them (default), the persistent kernel alone (CASR_GEMM16_TAIL=0) and
-    the per-tile kernel (CASR_GEMM16_PERSIST=0) give bitwise-identical encoder outputs (B = 256
-    and 128: 80 / 40 tiles past the last whole round; B = 37: 48 tiles in one partial round)."""
+    launch for the rows after them (default), the persistent kernel alone (CASR_OPT_GEMM16_TAIL = 0)
+    and the per-tile kernel (CASR_OPT_GEMM16_PERSIST = 0) give bitwise-identical encoder outputs
+    (B = 256 and 128: 80 / 40 tiles past the last whole round; B = 37: 48 tiles in one partial round)."""
     if eng.precision() != "s16x3":
         pytest.skip("the split-f16 input GEMM only")
     bind(eng, "peaked")
@@ -488,14 +511,16 @@ def test_input_gemm_tail_split_bitwise(eng, B, monkeypatch):
     frames = [800] * (B - 2) + [int(rs.randint(9, 800)), 9]
     fb, fr = batch_fbank(frames, eng.device)
     outs = []
-    for env in ({}, {"CASR_GEMM16_TAIL": "0"}, {"CASR_GEMM16_PERSIST": "0"}):
-        for k in ("CASR_GEMM16_TAIL", "CASR_GEMM16_PERSIST"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        eng.encode_fbank(fb, fr)
-        assert eng.device_flags() == 0
-        outs.append([t.cpu() for t in eng.encoder_results()])
+    try:
+        for tail, persist in ((1, 1), (0, 1), (1, 0)):
+            eng.set_option("GEMM16_TAIL", tail)
+            eng.set_option("GEMM16_PERSIST", persist)
+            eng.encode_fbank(fb, fr)
+            assert eng.device_flags() == 0
+            outs.append([t.cpu() for t in eng.encoder_results()])
+    finally:
+        eng.set_option("GEMM16_TAIL", 1)
+        eng.set_option("GEMM16_PERSIST", 1)
     for got in outs[1:]:
         for a, b in zip(outs[0], got):
             assert torch.equal(a, b)

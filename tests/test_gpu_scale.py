@@ -1,0 +1,216 @@
+"""HIP path vs the CPU oracle at the exact BASELINE.json sizes, the sharded (multi-GPU) product
+chain run shard by shard on one GPU, and beam search at a softmax temperature != 1.
+
+Sizes (BASELINE.json configs): the headline greedy B = 256, T = 800 (32 rows spread
+over the batch against the oracle), config 2 greedy B = 32, config 3 beam 8 at B = 128 (8
+utterances spread over the batch).  Weights are the bench recipe (proj x40 peaking, no EOS bias:
+all 40 decode steps run, so no early stop can differ between a sub-batch and the full batch; the
+reference is batch-invariant).  Tolerances as in test_gpu_parity.py: token ids
+identical, scores 2e-3 absolute.
+"""
+import functools
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import load_golden, fbank_for, golden_frames
+from oracle import casr_oracle as O
+from casr.config import CasrConfig
+from casr.lib import pack_weights
+from casr.results import greedy_outputs
+from casr.weights import synthetic_state_dicts
+
+pytestmark = pytest.mark.gpu
+
+CFG = CasrConfig()
+T_BENCH = 800
+G, META = load_golden()
+
+
+@functools.lru_cache(maxsize=None)
+def bench_weights():
+    return synthetic_state_dicts(CFG, peaked=True, eos_bias=0.0)
+
+
+@pytest.fixture(scope="module", params=["s16x3", "f32"])
+def eng(request):
+    from casr.engine import Engine
+    e = Engine(CFG, *bench_weights())
+    e.set_precision(request.param)
+    assert e.precision() == request.param
+    yield e
+    e.close()
+
+
+def _fbank(B, T=T_BENCH, first=0):
+    return np.stack([fbank_for(first + b, T) for b in range(B)])
+
+
+@functools.lru_cache(maxsize=None)
+def oracle_greedy(rows, T=T_BENCH):
+    feats = [O.features_from_fbank(fbank_for(b, T)) for b in rows]
+    return O.greedy_decode(feats, [f.shape[0] for f in feats], *bench_weights())
+
+
+@functools.lru_cache(maxsize=None)
+def oracle_beam(rows, k, T=T_BENCH):
+    feats = [O.features_from_fbank(fbank_for(b, T)) for b in rows]
+    return O.beam_decode(feats, [f.shape[0] for f in feats], *bench_weights(), k)
+
+
+def _greedy_rows_vs_oracle(eng, B, rows):
+    fb = torch.from_numpy(_fbank(B)).to(eng.device)
+    eng.encode_fbank(fb, torch.full((B,), T_BENCH, dtype=torch.int32, device=eng.device))
+    out = eng.greedy()
+    assert eng.device_flags() == 0
+    toks = out["tokens"].cpu().numpy()
+    acc = out["accum"].cpu().numpy()
+    r = oracle_greedy(tuple(rows))
+    np.testing.assert_array_equal(toks[list(rows)], r["all_tokens"])
+    np.testing.assert_allclose(acc[list(rows)], r["accum"], rtol=0, atol=2e-3)
+
+
+def test_headline_greedy_b256_rows_match_oracle(eng):
+    """North-star headline: greedy, B = 256, T = 800 (model.py:503-602), through casr_encode_fbank
+    as bench.py runs it; 32 rows spread over the whole batch (every row group of the recurrence,
+    every projection row block) token-exact against the oracle."""
+    _greedy_rows_vs_oracle(eng, 256, list(range(3, 256, 8)))
+
+
+def test_config2_greedy_b32_matches_oracle(eng):
+    """BASELINE config 2: greedy, B = 32, T = 800, every row against the oracle."""
+    _greedy_rows_vs_oracle(eng, 32, list(range(32)))
+
+
+def test_config3_beam8_b128_rows_match_oracle(eng):
+    """BASELINE config 3: beam 8 at B = 128 (R = 1024 decode rows: the 128-row decode GEMM
+    tiles and the beam tile-maxima select, model.py:604-987), T = 800; 8 utterances spread over the
+    batch against the oracle's beam search on those utterances: tokens identical, scores 2e-3."""
+    B, k = 128, 8
+    fb = torch.from_numpy(_fbank(B)).to(eng.device)
+    eng.encode_fbank(fb, torch.full((B,), T_BENCH, dtype=torch.int32, device=eng.device))
+    r = eng.beam(k)
+    assert eng.device_flags() == 0
+    toks, blen, sc = (x.cpu().numpy() for x in (r["tokens"], r["length"], r["score"]))
+    rows = (5, 21, 38, 60, 77, 94, 110, 127)
+    ref = oracle_beam(rows, k)
+    assert [toks[b, :blen[b]].tolist() for b in rows] == ref["tokens"]
+    np.testing.assert_allclose(sc[list(rows)], ref["score"], rtol=0, atol=2e-3)
+
+
+def test_metric_beam8_b256_batch_invariant(eng):
+    """The metric's beam shape, beam 8 at B = 256 (R = 2048 rows): equal to the same utterances
+    decoded as B = 128 batches (whose rows test_config3 pins to the oracle), bit for bit; two runs
+    are identical, and so are the attention's 8-rows-per-block default at this size and 4 rows per
+    block (CASR_OPT_ATTN_KPB)."""
+    B, k = 256, 8
+    fb = torch.from_numpy(_fbank(B)).to(eng.device)
+    fr = torch.full((B,), T_BENCH, dtype=torch.int32, device=eng.device)
+    eng.encode_fbank(fb, fr)
+    full = [x.cpu() for x in eng.beam(k).values()]
+    assert eng.device_flags() == 0
+    eng.encode_fbank(fb, fr)
+    again = [x.cpu() for x in eng.beam(k).values()]
+    try:
+        eng.set_option("ATTN_KPB", 4)
+        kpb4 = [x.cpu() for x in eng.beam(k).values()]
+    finally:
+        eng.set_option("ATTN_KPB", 0)
+    for a, b, c in zip(full, again, kpb4):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    for h in range(2):
+        eng.encode_fbank(fb[128 * h:128 * (h + 1)].contiguous(), fr[:128].contiguous())
+        r = eng.beam(k)
+        assert torch.equal(full[0][128 * h:128 * (h + 1)], r["tokens"].cpu())
+        assert torch.equal(full[1][128 * h:128 * (h + 1)], r["length"].cpu())
+        assert torch.equal(full[2][128 * h:128 * (h + 1)], r["score"].cpu())
+
+
+@pytest.mark.parametrize("name", ["plain", "peaked"])
+@pytest.mark.parametrize("k", [4, 8])
+def test_beam_temperature_matches_reference(name, k):
+    """gpd['temperature'] = 0.7 (model.py:834: logits / T before the log-softmax) against the
+    reference's own beam search captured at T = 0.7 (tests/golden/make_golden.py).  T != 1 takes
+    the select path that reads the full logit rows (beam_select_kernel<K2, false>: no projection
+    partials, they are of x, not x / T)."""
+    from casr.engine import Engine
+    cfg = CasrConfig(temperature=0.7)
+    frames = golden_frames(META)
+    for prec in ("s16x3", "f32"):
+        e = Engine(cfg, *synthetic_state_dicts(cfg, peaked=(name == "peaked")))
+        e.set_precision(prec)
+        try:
+            T = max(frames)
+            x = np.zeros((len(frames), T, 80), np.float32)
+            for b, t in enumerate(frames):
+                x[b, :t] = fbank_for(b, t)
+            feat, flen = e.features(torch.from_numpy(x).to(e.device),
+                                    torch.tensor(frames, dtype=torch.int32, device=e.device))
+            e.encode(feat, flen)
+            r = e.beam(k)
+            assert e.device_flags() == 0
+            toks, blen = r["tokens"].cpu().numpy(), r["length"].cpu().numpy()
+            gold = META[name][f"beam{k}_t07"]
+            assert [toks[b, :blen[b]].tolist() for b in range(len(frames))] == gold["tokens"], prec
+            np.testing.assert_allclose(r["score"].cpu().numpy(), gold["score"], rtol=0, atol=2e-3)
+        finally:
+            e.close()
+
+
+@pytest.mark.parametrize("B,k", [(256, 0), (64, 8)])
+def test_sharded_chain_equals_full_batch(B, k):
+    """The multi-GPU product chain (bench.py --gpus N) run shard by shard on one GPU:
+    rank 0 packs the blob -> the device copy every rank binds (what broadcast_packed delivers) ->
+    length-balanced partition into 4 shards -> per-shard Engine (one handle per "rank")
+    casr_encode_fbank + greedy (k = 0) or beam k + length weight -> merge_shards (what
+    gather_results assembles), against the single-batch decode; ragged lengths.
+      * Token ids are identical in every case (decisions are per utterance, model.py:570-578,
+        :897-901).
+      * Scores: bit for bit when the shards' decode-row counts fall in the full batch's decode-GEMM
+        tile class (greedy B = 256 -> ~64-row shards: 32-row LSTMCell and 64 x 80 projection blocks
+        either way).  Across tile classes (beam 8, B = 64: R = 512 rows against 128) the LSTMCell
+        splits its k loop over another number of waves, so the f32 sums round in another order:
+        scores within 2e-4 (measured 5e-5: sums of up to 40 log-probs plus length weight, ~40)."""
+    from casr.distributed import merge_shards, partition
+    from casr.engine import Engine
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
+    blob = torch.from_numpy(pack_weights(CFG, enc_sd, dec_sd)).to("cuda")
+    T = 420
+    rs = np.random.RandomState(17)
+    frames = rs.randint(60, T + 1, size=B).astype(np.int32)
+    x = np.zeros((B, T, 80), np.float32)
+    for b in range(B):
+        x[b, :frames[b]] = fbank_for(b, int(frames[b]))
+
+    def decode(e, idx):
+        fb = torch.from_numpy(x[idx]).to(e.device)
+        fr = torch.from_numpy(frames[idx]).to(e.device)
+        e.encode_fbank(fb, fr)
+        if k == 0:
+            g = e.greedy()
+            assert e.device_flags() == 0
+            toks, score = greedy_outputs(g["tokens"].cpu().numpy(), g["out_len"].cpu().numpy(),
+                                         g["finished"].cpu().numpy().astype(bool), g["accum"].cpu().numpy())
+            return [(toks[i], float(score[i])) for i in range(len(idx))]
+        r = e.beam(k, 1.5, 1.5)
+        assert e.device_flags() == 0
+        bt, bl, bs = (t.cpu().numpy() for t in (r["tokens"], r["length"], r["score"]))
+        return [(bt[i, :bl[i]].tolist(), float(bs[i])) for i in range(len(idx))]
+
+    full_eng = Engine(CFG, packed=blob)
+    full = decode(full_eng, np.arange(B))
+    full_eng.close()
+    parts = []
+    for idx in partition((frames // 3).tolist(), 4):
+        assert len(idx) > 0
+        e = Engine(CFG, packed=blob)
+        parts.append((idx, decode(e, idx)))
+        e.close()
+    merged = merge_shards(parts, B)
+    assert [m[0] for m in merged] == [f[0] for f in full]
+    got, ref = np.array([m[1] for m in merged]), np.array([f[1] for f in full])
+    if k == 0:
+        np.testing.assert_array_equal(got, ref)
+    else:
+        np.testing.assert_allclose(got, ref, rtol=0, atol=2e-4)

@@ -1,7 +1,10 @@
 """Host-side finalize rules (casr/results.py) against the reference semantics restated in the
 oracle and the reference-captured goldens: greedy score/length (model.py:582-593), loop
 length (model.py:578), finished-record ordering and second-pass selection (model.py:708-765)."""
+import os
+
 import numpy as np
+import pytest
 
 from golden_util import load_golden
 from casr.results import (edit_distance, get_wer, greedy_outputs, greedy_steps, records_by_utterance,
@@ -175,3 +178,36 @@ def test_manifest_and_eval_dataset_host(tmp_path):
         D.AudioDst(D.AudioBase(), mode="eval", dev_or_test="test")
     loader = D.AudioLoader(dst, batch_size=1)
     assert len(loader) == 2 and loader.loader is loader
+
+
+# ---------------------------------------------------------------- vocabulary (a13, data.py:373-374)
+DICT_PKL = "/root/reference/dict.pkl"
+DICT_PKL_SHA256 = "d81577bf8967efbfc587ad84e5653d95e2554ac980b469f1ca7814cce3b1d9d4"
+VOCAB_JSON_SHA256 = "513ac53677949db69de2bfb3f28c68d7e65c5fa2a09639e79bfb180372bde1dc"
+
+
+def test_vocab_json_pinned():
+    """The committed vocab.json (what the drop-in ships) is the table parsed from the reference's
+    dict.pkl in round 1: pinned by hash, 5004 contiguous ids with the reserved tokens first."""
+    import hashlib
+    from casr.vocab import VOCAB_JSON, load_vocab
+    with open(VOCAB_JSON, "rb") as f:
+        assert hashlib.sha256(f.read()).hexdigest() == VOCAB_JSON_SHA256
+    w2i, i2w = load_vocab()
+    assert len(i2w) == 5004 and sorted(i2w) == list(range(5004))
+    assert [i2w[i] for i in range(4)] == ["<pad>", "<s>", "</s>", "<unk>"]
+    assert all(w2i[w] == i for i, w in i2w.items())
+
+
+@pytest.mark.skipif(not os.path.exists(DICT_PKL), reason="reference dict.pkl only in the build container")
+def test_vocab_json_equals_reference_dict_pkl():
+    """Every entry of vocab.json and of its word2int against the reference's dict.pkl itself,
+    read by the opcode-level parser (nothing unpickled), whose bytes are pinned by sha256."""
+    import hashlib
+    from casr.vocab import load_dict_pkl, load_vocab
+    with open(DICT_PKL, "rb") as f:
+        assert hashlib.sha256(f.read()).hexdigest() == DICT_PKL_SHA256
+    w2i_ref, i2w_ref = load_dict_pkl(DICT_PKL)
+    w2i, i2w = load_vocab()
+    assert i2w == i2w_ref
+    assert w2i == w2i_ref
