@@ -196,6 +196,7 @@ def main():
                     help="MFMA arithmetic of the timed path (casr_set_precision)")
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the side measurement of the exact-f32 MFMA path")
+    ap.add_argument("--graphs", type=int, default=1, help="hipGraph replay of the decode loop (casr_set_graphs)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -232,6 +233,7 @@ def main():
     weight_s = time.perf_counter() - t_w
     eng = Engine(cfg, packed=packed, device=dev)
     eng.set_precision(args.precision)
+    eng.set_graphs(bool(args.graphs))
     precision = eng.precision()  # effective (f32 if the blob's s16 images are unusable)
 
     B, T = args.batch, args.frames
@@ -514,6 +516,7 @@ def main():
                                    f"encoder + 40-step attention decode, ids to host",
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
             "rtf": dt / args.steps / (B * world * AUDIO_S_PER_UTT),
+            "decode_launch": "hipGraph replay" if args.graphs else "eager launches",
             "beam": beam,
             "config3_beam8_b128": config3,
             "roofline": {"kernel": dominant, "bound": bound, "achieved": achieved, "peak": peak,

@@ -365,6 +365,7 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
   }
 }
 
+
 }  // namespace
 
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
@@ -401,8 +402,9 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     }
     const Order16 om{NB, NMm, NG};
     const int total = om.blocks();
-    hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin,
-                       std::min(M, NMm * G16_M), N, Kp, om, total, nk);
+    const int Mm = std::min(M, NMm * G16_M);
+    hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
+                       N, Kp, om, total, nk);
     if (NMm < NM) {
       const size_t r0 = (size_t)NMm * G16_M;
       const int Mt = M - (int)r0, NMt = (Mt + 127) / 128;

@@ -67,13 +67,10 @@ int main() {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char* names[8] = {"bias_kernel<4>", "persist", "p:no-dma", "p:iglp1", "p:prio", "p:iglp1+prio",
-                            "p:interleaved", "p:il no-dma"};
-    float* outs[8] = {dC0, dC1, dC1, dC1, dC1, dC1, dC1, dC1};
+    const char* names[6] = {"bias_kernel<4>", "persist", "p:no-dma", "p:iglp1", "p:prio", "p:iglp1+prio"};
+    float* outs[6] = {dC0, dC1, dC1, dC1, dC1, dC1};
     for (int rep = 0; rep < 3; ++rep)
-      for (int v = 0; v < 8; ++v) {
-        setenv("CASR_GEMM16_PERSIST", v ? "1" : "0", 1);
-        // the knob is read once per process: launch the kernels directly instead
+      for (int v = 0; v < 6; ++v) {
         const int NB = N / G16_N, NM = (M + G16_M - 1) / G16_M;
         int NG = 1;
         while (NG < 8 && NB % (NG * 2) == 0 && (size_t)(NB / NG) * G16_N * Kp * 4 > (3u << 20)) NG *= 2;
@@ -96,14 +93,8 @@ int main() {
           else if (v == 4)
             hipLaunchKernelGGL(gemm16_persist_kernel<16>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
                                order, order.blocks(), Kp / G16_K);
-          else if (v == 5)
-            hipLaunchKernelGGL(gemm16_persist_kernel<24>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks(), Kp / G16_K);
-          else if (v == 6)
-            hipLaunchKernelGGL(gemm16_persist_kernel<32>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
-                               order, order.blocks(), Kp / G16_K);
           else
-            hipLaunchKernelGGL(gemm16_persist_kernel<33>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
+            hipLaunchKernelGGL(gemm16_persist_kernel<24>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
                                order, order.blocks(), Kp / G16_K);
         }
         CK(hipEventRecord(e1));
@@ -113,11 +104,7 @@ int main() {
         const double flop = 2.0 * M * N * (double)Kp * 3;
         printf("Kp %d %-16s %8.1f us  %6.0f TF/s f16\n", Kp, names[v], 1000.0 * ms / iters, flop / (ms / iters * 1e-3) / 1e12);
       }
-    // the bitwise check needs the persist result: rerun it last (CHECK_IL=1: the interleaved one)
-    if (getenv("CHECK_IL"))
-      hipLaunchKernelGGL(gemm16_persist_kernel<32>, dim3(256), dim3(512), 0, 0, dA, dW, dB, dC1, M, N, Kp,
-                         Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}, Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}.blocks(), Kp / G16_K);
-    else
+    // the bitwise check needs the persist result: rerun it last
     hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(256), dim3(512), 0, 0, dA, dW, dB, dC1, M, N, Kp,
                        Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}, Order16{N / G16_N, (M + G16_M - 1) / G16_M, 2}.blocks(), Kp / G16_K);
     CK(hipDeviceSynchronize());

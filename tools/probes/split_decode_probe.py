@@ -28,8 +28,12 @@ def main():
     fb = torch.from_numpy(np.stack([np.random.RandomState(1234 + b).standard_normal((T, 80)).astype(np.float32)
                                     for b in range(B)])).to(dev)
     fr = torch.full((B,), T, dtype=torch.int32, device=dev)
+    graphs = os.environ.get("GRAPHS", "0") == "1"
     full = Engine(cfg, packed=blob, device=dev)
     halves = [Engine(cfg, packed=blob, device=dev) for _ in range(2)]
+    for e in [full] + halves:
+        e.set_graphs(graphs)
+    print("graphs", graphs, flush=True)
     full.encode_fbank(fb, fr)
     for h, e in enumerate(halves):
         e.encode_fbank(fb[128 * h:128 * (h + 1)].contiguous(), fr[:128].contiguous())
