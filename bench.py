@@ -60,8 +60,8 @@ def kernel_work(cls, B, Tp, R, V, T):
         return 40 * 2.0 * R * V * (C + HD), "mfma"
     if cls == "attention":   # keys + values streamed once per utterance per step
         return 40 * 4.0 * B * Tp * (A + C), "hbm"
-    if cls == "select":
-        return 40 * 4.0 * R * V, "hbm"
+    if cls == "select":      # the greedy select reads ProjA's per-block (max, sum, argmax) partials,
+        return 40 * 4.0 * 3 * R * 64, "hbm"  # never the [R, V] logits (fused select: one launch)
     if cls == "features":    # fbank read + the layer-0 s16 row image written (Kp = 768: 4 B per column)
         return 4.0 * B * (T * 80 + Tp * 768), "hbm"
     return 0.0, "hbm"
@@ -196,7 +196,8 @@ def main():
                     help="MFMA arithmetic of the timed path (casr_set_precision)")
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the side measurement of the exact-f32 MFMA path")
-    ap.add_argument("--graphs", type=int, default=1, help="hipGraph replay of the decode loop (casr_set_graphs)")
+    ap.add_argument("--graphs", type=int, default=0,
+                    help="1: hipGraph replay of the decode loop (casr_set_graphs); default 0: eager launches")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -233,7 +234,7 @@ def main():
     weight_s = time.perf_counter() - t_w
     eng = Engine(cfg, packed=packed, device=dev)
     eng.set_precision(args.precision)
-    eng.set_graphs(bool(args.graphs))
+    eng.set_graphs(2 | (1 if args.graphs else 0))
     precision = eng.precision()  # effective (f32 if the blob's s16 images are unusable)
 
     B, T = args.batch, args.frames

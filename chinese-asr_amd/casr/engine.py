@@ -191,8 +191,11 @@ class Engine:
         return f.value
 
     def set_graphs(self, enable):
-        """hipGraph replay of the launch-bound loops (default on); off = eager launches."""
-        _lib.check(self.lib.casr_set_graphs(self.handle, int(bool(enable))), self.handle)
+        """hipGraph replay of the launch-bound loops: True = decode loop and per-step recurrence
+        fallback, False = both eager, or an int mode (include/casr.h CASR_GRAPHS_*; default 2:
+        decode eager, recurrence fallback replayed)."""
+        mode = (3 if enable else 0) if isinstance(enable, bool) else int(enable)
+        _lib.check(self.lib.casr_set_graphs(self.handle, mode), self.handle)
 
     def set_persistent(self, enable):
         """Persistent per-layer recurrence (default on where its grid fits); off = per-step."""

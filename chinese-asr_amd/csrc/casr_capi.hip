@@ -185,7 +185,9 @@ struct casr_handle {
   int dec_k = 0;
   bool beam_done = false;
   // hipGraph replay of the launch-bound loops (per-layer recurrence, decode loop)
-  bool use_graphs = true;
+  // casr_set_graphs bits: 1 = the decode loop replays as a hipGraph, 2 = the per-step recurrence
+  // fallback does.  Default 2: the decode loop launches eagerly (measured faster)
+  int graph_mode = CASR_GRAPHS_RECURRENCE;
   hipStream_t cap = nullptr;      // capture stream
   hipStream_t xs[2] = {};         // replay streams, fenced to the caller's stream by events
   hipEvent_t ev_in = nullptr, ev_out[2] = {};
@@ -472,7 +474,8 @@ void casr_destroy(casr_handle* h) {
 
 int casr_set_graphs(casr_handle* h, int enable) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
-  h->use_graphs = enable != 0;
+  if (enable < 0 || enable > 3) return fail(h, CASR_ERR_ARG, "casr_set_graphs: mode %d not in [0, 3]", enable);
+  h->graph_mode = enable;
   return CASR_OK;
 }
 
@@ -709,7 +712,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
       }
       return e;
     };
-    if (h->use_graphs) {
+    if (h->graph_mode & CASR_GRAPHS_RECURRENCE) {
       // rows are independent: two row halves replay as two graphs on two streams, so one
       // half's load latency hides behind the other's MFMAs
       const int nsplit = B >= 64 ? 2 : 1;
@@ -806,7 +809,7 @@ int casr_encoder_results(casr_handle* h, float* enc, float* h_final, float* c_fi
 static bool decode_graph_ok(const casr_handle* h) {
   const uint32_t dec = (1u << CASR_K_DEC_LSTM) | (1u << CASR_K_ATTENTION) | (1u << CASR_K_PROJ) |
                        (1u << CASR_K_SELECT);
-  return h->use_graphs && !(h->prof.mask & dec);
+  return (h->graph_mode & CASR_GRAPHS_DECODE) && !(h->prof.mask & dec);
 }
 
 static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {

@@ -247,10 +247,14 @@ enum {
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);
 
-/* The launch-bound loops (each layer's Tp recurrence steps, the whole decode loop) are
- * captured once per shape into hipGraphs on a private stream and replayed on `stream`
- * (default on).  0 = launch every kernel eagerly (same results, bit for bit). */
-int casr_set_graphs(casr_handle* h, int enable);
+/* hipGraph replay of the launch-bound loops: bit CASR_GRAPHS_DECODE = the whole decode loop,
+ * bit CASR_GRAPHS_RECURRENCE = each layer's Tp steps of the per-step recurrence fallback; each
+ * loop is captured once per shape on a private stream and replayed on `stream`, else its kernels
+ * launch eagerly on `stream` (same results, bit for bit).  Default CASR_GRAPHS_RECURRENCE: the
+ * decode loop launches eagerly, measured 0.1 ms faster per greedy batch and 0.17 ms per beam
+ * batch than its replay (round 3; the host enqueues ~160 launches well ahead of the device). */
+enum { CASR_GRAPHS_DECODE = 1, CASR_GRAPHS_RECURRENCE = 2 };
+int casr_set_graphs(casr_handle* h, int mode);
 
 /* Launch timing per kernel class with HIP event pairs recorded on the launch stream around
  * every launch of the enabled classes (bench.py's roofline figures).  Enabling resets

@@ -216,7 +216,7 @@ def test_graph_replay_equals_eager(eng):
         assert eng.device_flags() == 0
         outs.append((enc, g["tokens"].cpu(), g["accum"].cpu(), g["alignment"].cpu(), bm["tokens"].cpu(),
                      bm["score"].cpu(), bm["steps"].cpu()))
-    eng.set_graphs(True)
+    eng.set_graphs(2)  # the default: decode eager, recurrence fallback replayed
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
     for a, b in zip(outs[1], outs[2]):
@@ -258,7 +258,7 @@ def test_fused_select_equals_select_launches(eng, eos_bias, graphs):
                 eng.profile([])
     finally:
         eng.set_option("FUSE_SELECT", 1)
-        eng.set_graphs(True)
+        eng.set_graphs(2)
     assert outs[0].keys() == outs[1].keys() and "tokens" in outs[0]
     for o in outs[1:]:
         for k in outs[0]:

@@ -16,15 +16,18 @@ import os
 import sys
 from collections import defaultdict
 
-CLASS_OF = {  # bench.py kernel classes -> kernel-name prefixes (after short())
-    "input_proj": "gemm16_bias_kernel",
-    "keys": "gemm_nt_kernel<KeysEpi>",
-    "rec_step": "rec_layer_kernel",
-    "dec_lstm": "dgemm_kernel<2, 4, 4, DecLstmA",
-    "proj": "dgemm_kernel<4, 5, 4, ProjA",
-    "attention": "attention_kernel<1>",
-    "select": "greedy_select_part_kernel",
-    "features": "features_rows_kernel<true>",
+# bench.py kernel classes -> (kernel-name prefixes after short(), launches of the class per step
+# as bench.py counts them: one "launch" of input_proj = one layer's projection, persistent kernel
+# and half-tile tail together)
+CLASS_OF = {
+    "input_proj": (("gemm16_persist_kernel", "gemm16_bias_kernel"), 4),
+    "rec_step": (("rec_layer_kernel",), 4),
+    "keys": (("gemm_nt_kernel<KeysEpi",), 1),
+    "dec_lstm": (("dgemm_kernel<2, 4, 4, DecLstmA", "dgemm_kernel<4, 4, 4, DecLstmA", "dgemm_kernel<8, 4, 3, DecLstmA"), 40),
+    "proj": (("dgemm_kernel<2, 5, 4, ProjA", "dgemm_kernel<4, 5, 4, ProjA", "dgemm_kernel<8, 5, 3, ProjA",
+              "dgemm_kernel<4, 10, 2, ProjA"), 40),
+    "attention": (("attention_kernel",), 40),
+    "features": (("features_stats_kernel", "features_rows_kernel"), 1),
 }
 
 
@@ -69,11 +72,25 @@ def main(d, json_out=None):
         write = a["WRITE_SIZE"] / 1024 if "WRITE_SIZE" in a else float("nan")
         print(f"{name[:52]:52s} {grid:8d} {n:4d} {us:8.1f} {clk:6.2f} {mf:6.1f} {wait:6.1f} {stall:6.1f} {lds:5.1f} "
               f"{fetch:8.2f} {write:8.2f}")
-        for cls, pre in CLASS_OF.items():
-            if name.startswith(pre) and cls not in traffic and fetch == fetch:
-                traffic[cls] = {"fetch_bytes": fetch * 1e6 * 1.048576, "write_bytes": write * 1e6 * 1.048576,
-                                "hbm_bytes": (fetch + (write if write == write else 0)) * 1048576.0,
-                                "grid": grid, "note": "per launch, FETCH_SIZE x2 (gfx950) + WRITE_SIZE"}
+    # per class: every dispatch of its kernels summed over the run, then per bench launch
+    steps = int(os.environ.get("STEPS", 2))
+    for cls, (pres, per_step) in CLASS_OF.items():
+        tot = defaultdict(float)
+        for (name, grid), cs in per.items():
+            if any(name.startswith(p) for p in pres):
+                for c, v in cs.items():
+                    tot[c] += sum(v)
+        if "FETCH_SIZE" not in tot:
+            continue
+        launches = steps * per_step
+        fetch = 2 * tot["FETCH_SIZE"] * 1024 / launches  # KB -> B, gfx950 x2
+        write = tot.get("WRITE_SIZE", 0.0) * 1024 / launches
+        rec = {"fetch_bytes": fetch, "write_bytes": write, "hbm_bytes": fetch + write,
+               "launches_per_step": per_step,
+               "note": "per bench launch: all dispatches of the class summed, FETCH_SIZE x2 (gfx950) + WRITE_SIZE"}
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in tot and tot.get("GRBM_GUI_ACTIVE"):
+            rec["mfma_busy"] = tot["SQ_VALU_MFMA_BUSY_CYCLES"] / (tot["GRBM_GUI_ACTIVE"] / 8 * 1024)
+        traffic[cls] = rec
     if json_out:
         json.dump(traffic, open(json_out, "w"), indent=1)
         print("wrote", json_out)

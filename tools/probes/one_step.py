@@ -1,5 +1,5 @@
-"""One warm greedy step at the headline config (B=256, T=800) for PMC collection (rocprofv3
---pmc passes); runs the same launches as one bench.py step.  BEAM=k: a beam step instead (set B
+"""STEPS (default 2) greedy steps at the headline config (B=256, T=800) for PMC collection
+(rocprofv3 --pmc passes); runs the same launches as bench.py's step (casr_encode_fbank, greedy).  BEAM=k: a beam step instead (set B
 too, e.g. B=128 BEAM=8 for the bench's beam line)."""
 import os
 import sys
@@ -20,8 +20,7 @@ fb = torch.from_numpy(np.stack([np.random.RandomState(1234 + b).standard_normal(
                                 for b in range(B)])).cuda()
 frames = torch.full((B,), T, dtype=torch.int32, device="cuda")
 for _ in range(int(os.environ.get("STEPS", 2))):
-    feat, flen = eng.features(fb, frames)
-    eng.encode(feat, flen)
+    eng.encode_fbank(fb, frames)  # as bench.py's step: features straight into the layer-0 image
     if int(os.environ.get("BEAM", 0)):
         eng.beam(int(os.environ["BEAM"]))
     else:

@@ -1,0 +1,22 @@
+# Round-3 evidence on one box (profiles/r03): the default bench line; rocprofv3 kernel trace +
+# stats of a greedy-only bench run (its dominant kernel's average must agree with the line's
+# HIP-event figure: 20 timed steps dominate the 3 untimed ones); PMC passes of two greedy steps.
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/r03
+mkdir -p $O
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+python -c "import json; d=json.load(open('$O/bench.json')); print('bench', round(d['value']), round(d['ms_per_step'],3), d['roofline']['avg_launch_us'], d['beam']['ms_per_step'])"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+  python3 bench.py --steps 20 --warmup 2 --no-beam --no-configs --no-f32-compare --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err || { tail -5 $O/prof.err; exit 1; }
+python tools/prof_by_grid.py $O/prof/run_kernel_trace.csv 30 > $O/prof_by_grid.txt 2>&1
+head -12 $O/prof_by_grid.txt
+R=$GRAFT_REPO_ROOT
+P=$O/pmc
+mkdir -p $P
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d $P/p1 -o p1 -- python3 $R/tools/probes/one_step.py > $P/p1.log 2>&1 || { tail -3 $P/p1.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/p2 -o p2 -- python3 $R/tools/probes/one_step.py > $P/p2.log 2>&1 || { tail -3 $P/p2.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/p3 -o p3 -- python3 $R/tools/probes/one_step.py > $P/p3.log 2>&1 || { tail -3 $P/p3.log; exit 1; }
+python tools/pmc_summary.py $P --json $O/pmc_traffic.json > $O/pmc_summary.txt 2>&1
+head -14 $O/pmc_summary.txt
+cat $O/pmc_traffic.json | head -50
