@@ -7,6 +7,9 @@ O=gpurun_out/r03
 mkdir -p $O
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
 python -c "import json; d=json.load(open('$O/bench.json')); print('bench', round(d['value']), round(d['ms_per_step'],3), d['roofline']['avg_launch_us'], d['beam']['ms_per_step'])"
+# the profiled runs launch the recurrence without hipLaunchCooperativeKernel (same kernel, same
+# grid; a cooperative-launch process crashed at exit under rocprofv3 in round 3)
+export CASR_OPTS=REC_COOP=0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
   python3 bench.py --steps 20 --warmup 2 --no-beam --no-configs --no-f32-compare --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err || { tail -5 $O/prof.err; exit 1; }
 python tools/prof_by_grid.py $O/prof/run_kernel_trace.csv 30 > $O/prof_by_grid.txt 2>&1
