@@ -14,6 +14,8 @@
 // rounded up to 4) so a lane reads 4 consecutive time steps of one key row.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "casr_common.h"
 #include "casr_internal.h"
 
@@ -21,7 +23,7 @@ namespace casr {
 
 constexpr int AT_THREADS = 512;
 constexpr int AT_WAVES = AT_THREADS / 64;
-constexpr int AT_NQ = HD / 16;  // query partials per row (one per 16-unit block of h)
+constexpr int AT_NQ = HD / 16;  // query partials per row at most (dec_q_slots: one per LSTMCell column block)
 constexpr int AT_MAXG = 8;      // a-groups of the score phase
 constexpr int AT_CH = 20;       // keys rows in flight per score batch (apg = 19 at Tp = 266)
 constexpr int AT_APAD = A + AT_CH;  // q / v rows in LDS, zero-padded so a batch never branches
@@ -34,10 +36,26 @@ __host__ __device__ constexpr int attn_scratch_floats(int Tq) {
   return AT_MAXG * KPB * Tq > 4 * KPB * C ? AT_MAXG * KPB * Tq : 4 * KPB * C;
 }
 
+// LDS: qs, eqs [AT_APAD][KPB] | vs, v2s [A] | (AT_MAXG unused) | scratch | es [Tq][KPB] | value rows
 template <int KPB>
 __host__ __device__ constexpr size_t attn_smem_floats(int Tp) {
-  return (size_t)KPB * AT_APAD + AT_APAD + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp);
+  return (size_t)2 * KPB * AT_APAD + 2 * A + AT_MAXG + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp);
 }
+
+// Split exponential form of the score tanh.  tanh(k + q) = 1 - 2 / (1 + e^{2k} e^{2q}): with
+// ek = exp(2k) computed once per encode (KeysEpi, next to the keys) and eq = exp(2q) once per row
+// and step, a term costs one fma (d = ek eq + 1), one v_rcp_f32 and one fma into the score,
+// against two transcendentals in tanh_fast.  The score of an a-group is
+//     sum_a v_a tanh(k_a + q_a) = sum_a v_a  +  sum_a (-2 v_a) / (1 + ek_a eq_a).
+// Range: ek and eq are finite normal floats while |k|, |q| < 43 (exp2 of up to 124); their product
+// then overflows to +inf only where k + q > 44 (rcp = 0, tanh = 1, as tanh_fast) and underflows
+// only where k + q < -51 (d = 1, tanh = -1).  Outside that range ek / eq are stored as NaN, which
+// makes the block's score NaN and sends the block back to the direct form (also the path for a
+// NaN key or query, whose scores then come out as in tanh_fast).  Error: the exponent products
+// round k 2 log2(e) and q 2 log2(e) separately, so e^{2k} e^{2q} carries ~1.2e-7 (|k| + |q|)
+// relative error where exp(2(k + q)) carries ~1.2e-7 |k + q|; for the |k|, |q| of a few units of
+// the path's activations the score moves by ~1e-6 at most (tests: alignment within 1e-5).
+// split_exp2x: casr_common.h (shared with KeysEpi)
 
 // tanh(x) = 1 - 2 / (1 + exp(2x)) on v_exp_f32 / v_rcp_f32: mul, exp, add, rcp, fma (5 VALU
 // ops; the libm-style division __fdividef compiles to on gfx950 is an 11-instruction
@@ -74,10 +92,10 @@ __device__ uint32_t* g_at_trace = nullptr;
 template <int KPB>
 __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float* __restrict__ st, const float* __restrict__ qpart, const float* __restrict__ keysT,
-    const float* __restrict__ enc, const int32_t* __restrict__ lens, const float* __restrict__ vv, int R, int k,
-    int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone, int l, int total, int npf) {
+    const float* __restrict__ ekT, const float* __restrict__ enc, const int32_t* __restrict__ lens,
+    const float* __restrict__ vv, int R, int k, int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone,
+    int l, int total, int npf, int direct, int nq) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  __shared__ float wred[2][AT_WAVES][KPB];
   uint32_t* atr = g_at_trace ? g_at_trace + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int i) {
     if (atr && threadIdx.x == 0) atr[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -85,9 +103,11 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   stamp(0);
   if (done_before(newdone, l) >= total) return;
   const int Tq = attn_tq(Tp);
-  float* qs = sm;                  // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
-  float* vs = qs + KPB * AT_APAD;  // [AT_APAD], zero past A
-  float* xs = vs + A;              // scratch
+  float* qs = sm;                   // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
+  float* eqs = qs + KPB * AT_APAD;  // [AT_APAD][KPB]: exp(2q) (split form), zero past A
+  float* vs = eqs + KPB * AT_APAD;  // [A]
+  float* v2s = vs + A;              // [A]: -2 v
+  float* xs = v2s + A + AT_MAXG;    // scratch
   float* es = xs + attn_scratch_floats<KPB>(Tq);  // [Tq][KPB]: one 4 x KPB-byte read per t
   float* vl = es + KPB * Tq;                       // [npf][C]: value rows 0..npf-1 (LDS-DMA)
   const int b = blockIdx.x, j0 = blockIdx.y * KPB;
@@ -96,43 +116,66 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   const int len = min(lens[b], Tp);
   const size_t row0 = (size_t)b * k + j0;
 
-  // 1. q = sum of the HD/16 partials (fixed order), v -> LDS
-  // (KPB x A = 128 KPB items: one round of 16 loads per thread at KPB <= 4; the zero pad rows
-  // a >= A take no loads)
-  for (int i = tid; i < KPB * A; i += AT_THREADS) {
-    const int j = i / A, a = i - j * A;
-    float q = 0.f;
+  // 1. q = sum of the HD/16 partials in partial order (p = 0, 1, ...), v -> LDS.  The block's
+  // KPB rows are consecutive, so partial p of all of them is one contiguous KPB x A span: a thread
+  // takes one float4 (row j, columns 4 a4..4 a4 + 3) and has its AT_NQ 16-B loads in flight at
+  // once (one round trip; the zero pad rows a >= A take no loads)
+  for (int f = tid; f < KPB * (A / 4); f += AT_THREADS) {
+    const int j = f / (A / 4), a4 = f - j * (A / 4);
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     if (j < nk) {
-      const float* qp = qpart + (row0 + j) * A + a;
-      float pv[AT_NQ];
+      const float4* qp = reinterpret_cast<const float4*>(qpart + (row0 + j) * A) + a4;
+      float4 pv[AT_NQ];
 #pragma unroll
-      for (int p = 0; p < AT_NQ; ++p) pv[p] = qp[(size_t)p * R * A];
+      for (int p = 0; p < AT_NQ; ++p) pv[p] = p < nq ? qp[(size_t)p * R * (A / 4)] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int p = 0; p < AT_NQ; ++p) q += pv[p];
+      for (int p = 0; p < AT_NQ; ++p)
+        if (p < nq) q.x += pv[p].x, q.y += pv[p].y, q.z += pv[p].z, q.w += pv[p].w;
     }
-    qs[a * KPB + j] = q;
+    qs[(4 * a4 + 0) * KPB + j] = q.x;
+    qs[(4 * a4 + 1) * KPB + j] = q.y;
+    qs[(4 * a4 + 2) * KPB + j] = q.z;
+    qs[(4 * a4 + 3) * KPB + j] = q.w;
+    eqs[(4 * a4 + 0) * KPB + j] = j < nk ? split_exp2x(q.x) : 0.f;
+    eqs[(4 * a4 + 1) * KPB + j] = j < nk ? split_exp2x(q.y) : 0.f;
+    eqs[(4 * a4 + 2) * KPB + j] = j < nk ? split_exp2x(q.z) : 0.f;
+    eqs[(4 * a4 + 3) * KPB + j] = j < nk ? split_exp2x(q.w) : 0.f;
   }
-  for (int i = tid; i < KPB * (AT_APAD - A); i += AT_THREADS) qs[A * KPB + i] = 0.f;
-  if (tid < AT_APAD) vs[tid] = tid < A ? vv[tid] : 0.f;
+  for (int i = tid; i < KPB * (AT_APAD - A); i += AT_THREADS) qs[A * KPB + i] = eqs[A * KPB + i] = 0.f;
+  // score work split: G a-groups of apg keys rows x Tq / 4 chunks of 4 steps
+  const int nch = Tq / 4;
+  const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
+  const int apg = (A + G - 1) / G;
+  if (tid < A) {
+    const float v = vv[tid];
+    vs[tid] = v;
+    v2s[tid] = -2.f * v;
+  }
   __syncthreads();
   stamp(1);
 
   // 2. scores.  Thread = (a-group ag, 4-step chunk c): its APG keys rows' float4 at chunk c are
   // all loaded before use; partial sums per a-group go to LDS and are added in group order.
-  const int nch = Tq / 4;
-  const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
-  const int apg = (A + G - 1) / G;
+  // Split form (ekT, see split_exp2x) unless `direct` or a NaN score sends the block back to the
+  // direct tanh(k + q) over keysT.
   const float* kb = keysT + (size_t)b * A * Tq;
+  const float* ekb = ekT + (size_t)b * A * Tq;
   constexpr int CH = KPB >= 8 ? AT_CH / 2 : AT_CH;  // KPB 8: half the keys rows per batch (registers)
   // this thread's score work: (a-group, 4-step chunk) items it = tid, tid + 512, ...; each in
   // batches of CH keys rows
-  auto score_item = [&](int it, bool first, auto&& after_loads) {
+  bool nan_seen = false;  // a NaN score of this thread's items (split form: leave it to the direct form)
+  auto score_item = [&](int it, bool first, auto&& after_loads, auto SPLIT) {
+    constexpr bool split = decltype(SPLIT)::value;
     const int ag = it / nch, c = it - ag * nch, t0 = 4 * c;
     const int a0 = ag * apg, a1 = min(A, a0 + apg);
     const bool live = it < G * nch && t0 < len;
+    const float* src = split ? ekb : kb;
     float e4[KPB][4];
+    float e0 = 0.f;  // split form: the score starts at the group's sum of v (a order, from LDS)
+    if (split && live)
+      for (int a = a0; a < a1; ++a) e0 += vs[a];
 #pragma unroll
-    for (int j = 0; j < KPB; ++j) e4[j][0] = e4[j][1] = e4[j][2] = e4[j][3] = 0.f;
+    for (int j = 0; j < KPB; ++j) e4[j][0] = e4[j][1] = e4[j][2] = e4[j][3] = e0;
     // branch-free: a slot past the group's last row gets v = 0 (its keys load is zero-filled and
     // q is padded), so it adds an exact zero and the real terms keep their order; rows j >= nk
     // compute on q = 0 and are never stored
@@ -140,6 +183,25 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     // is within the attention tolerance either way; hipcc already contracted the former
     // round-to-nearest intrinsic pairs into these FMAs)
     auto batch = [&](const float4 (&kv)[CH], int ab) {
+      if constexpr (split) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const float vm = ab + i < a1 ? v2s[ab + i] : 0.f;
+#pragma unroll
+          for (int j = 0; j < KPB; ++j) {
+            const float ea = eqs[(ab + i) * KPB + j];
+            const f32x2 e2 = {ea, ea}, v2 = {vm, vm}, one = {1.f, 1.f};
+            const f32x2 dlo = __builtin_elementwise_fma((f32x2){kv[i].x, kv[i].y}, e2, one);
+            const f32x2 dhi = __builtin_elementwise_fma((f32x2){kv[i].z, kv[i].w}, e2, one);
+            const f32x2 rlo = {__builtin_amdgcn_rcpf(dlo.x), __builtin_amdgcn_rcpf(dlo.y)};
+            const f32x2 rhi = {__builtin_amdgcn_rcpf(dhi.x), __builtin_amdgcn_rcpf(dhi.y)};
+            const f32x2 a01 = __builtin_elementwise_fma(rlo, v2, (f32x2){e4[j][0], e4[j][1]});
+            const f32x2 a23 = __builtin_elementwise_fma(rhi, v2, (f32x2){e4[j][2], e4[j][3]});
+            e4[j][0] = a01.x, e4[j][1] = a01.y, e4[j][2] = a23.x, e4[j][3] = a23.y;
+          }
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const float va = ab + i < a1 ? vs[ab + i] : 0.f;
@@ -158,7 +220,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     auto load = [&](float4 (&kv)[CH], int ab) {
 #pragma unroll
       for (int i = 0; i < CH; ++i)
-        kv[i] = live && ab + i < a1 ? *reinterpret_cast<const float4*>(kb + (size_t)(ab + i) * Tq + t0)
+        kv[i] = live && ab + i < a1 ? *reinterpret_cast<const float4*>(src + (size_t)(ab + i) * Tq + t0)
                                     : make_float4(0.f, 0.f, 0.f, 0.f);
     };
     int ab = a0;
@@ -177,15 +239,21 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     if (live)
 #pragma unroll
       for (int j = 0; j < KPB; ++j)
-        if (j < nk)
+        if (j < nk) {
           *reinterpret_cast<float4*>(xs + (ag * KPB + j) * Tq + t0) = make_float4(e4[j][0], e4[j][1], e4[j][2], e4[j][3]);
+          if (split)  // steps past len are masked (their keysT / ekT slots may hold anything)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) nan_seen |= t0 + q < len && e4[j][q] != e4[j][q];
+        }
   };
+  using SplitT = std::true_type;
+  using DirectT = std::false_type;
   // The first batch of keys is loaded and waited for by every wave (a wait hipcc sees), then the
   // value rows 0..npf-1 go to LDS by LDS-DMA (inline asm, hipcc does not see it) and stream in
   // while the block computes tanh scores and the softmax: the chip's HBM is otherwise idle in
   // those phases, since every block runs them at the same time.
   const int nv = min(npf, len);
-  score_item(tid, true, [&]() {
+  auto value_dma = [&]() {
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): the keys batch has landed
     const uint32_t vbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)vl;
     for (int i = wv; i < 2 * nv; i += AT_WAVES) {  // 1 KB (half a row) per wave instruction
@@ -197,80 +265,118 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
                    : "v"(src), "s"(dst)
                    : "memory");
     }
-  });
-  for (int it = tid + AT_THREADS; it < G * nch; it += AT_THREADS) score_item(it, false, [] {});
-  __syncthreads();
+  };
+  if (!direct) {
+    score_item(tid, true, value_dma, SplitT{});
+    for (int it = tid + AT_THREADS; it < G * nch; it += AT_THREADS) score_item(it, false, [] {}, SplitT{});
+  }
+  // direct form: requested, or a NaN score in the block (every thread redoes its own items)
+  if (__syncthreads_or(direct || nan_seen)) {
+    if (direct) score_item(tid, true, value_dma, DirectT{});
+    else score_item(tid, false, [] {}, DirectT{});
+    for (int it = tid + AT_THREADS; it < G * nch; it += AT_THREADS) score_item(it, false, [] {}, DirectT{});
+    __syncthreads();
+  }
   stamp(2);
 
-  // combine the G group partials (fixed order), mask past len, row maxima
-  float lmax[KPB];
+  // 3. masked softmax over t (torch: exp(x - max), sum, then * 1/sum), one wave per row (KPB <= 8
+  // waves): the G group partials combined in group order, the row maximum and the sum by wave
+  // reductions, no block barrier until the context phase.  Lane ln takes t = ln, ln + 64, ... in
+  // every pass, so a row's arithmetic is the same at every KPB.
+  // KPB <= 2 (greedy, k = 2): every thread takes a t and the reductions go through LDS (with one
+  // or two rows a single wave's three lane-strided passes were slower: 2.3 against 1.2 us)
+  static_assert(KPB <= AT_WAVES, "one wave per beam row of the block");
+  if constexpr (KPB <= 2) {
+    __shared__ float wred[2][AT_WAVES][KPB];
+    float lmax[KPB];
 #pragma unroll
-  for (int j = 0; j < KPB; ++j) {
-    lmax[j] = -INFINITY;
-    if (j < nk)
-      for (int t = tid; t < Tq; t += AT_THREADS) {
-        float ev = -INFINITY;
-        if (t < len) {
-          const float* x = xs + j * Tq + t;
-          const int gs = KPB * Tq;
-          ev = x[0];
-          for (int gg = 1; gg < G; ++gg) ev += x[gg * gs];
+    for (int j = 0; j < KPB; ++j) {
+      lmax[j] = -INFINITY;
+      if (j < nk)
+        for (int t = tid; t < Tq; t += AT_THREADS) {
+          float ev = -INFINITY;
+          if (t < len) {
+            const float* x = xs + j * Tq + t;
+            const int gs = KPB * Tq;
+            ev = x[0];
+            for (int gg = 1; gg < G; ++gg) ev += x[gg * gs];
+          }
+          es[t * KPB + j] = ev;
+          lmax[j] = fmaxf(lmax[j], ev);
         }
-        es[t * KPB + j] = ev;
-        lmax[j] = fmaxf(lmax[j], ev);
-      }
-  }
-#pragma unroll
-  for (int j = 0; j < KPB; ++j)
-    if (j < nk) {
-      const float m = wave_max(lmax[j]);
-      if (ln == 0) wred[0][wv][j] = m;
     }
-  __syncthreads();
-  float rmax[KPB], lsum[KPB];
 #pragma unroll
-  for (int j = 0; j < KPB; ++j) {
+    for (int j = 0; j < KPB; ++j)
+      if (j < nk) {
+        const float m = wave_max(lmax[j]);
+        if (ln == 0) wred[0][wv][j] = m;
+      }
+    __syncthreads();
+    float rmax[KPB], lsum[KPB];
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) {
+      float m = -INFINITY;
+      if (j < nk)
+#pragma unroll
+        for (int w = 0; w < AT_WAVES; ++w) m = fmaxf(m, wred[0][w][j]);
+      rmax[j] = m;
+      lsum[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < KPB; ++j)
+      if (j < nk)
+        for (int t = tid; t < Tq; t += AT_THREADS) {
+          const float p = expf(es[t * KPB + j] - rmax[j]);
+          es[t * KPB + j] = p;
+          lsum[j] += p;
+        }
+#pragma unroll
+    for (int j = 0; j < KPB; ++j)
+      if (j < nk) {
+        const float s = wave_sum(lsum[j]);
+        if (ln == 0) wred[1][wv][j] = s;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < KPB; ++j)
+      if (j < nk) {
+        const float s = ((wred[1][0][j] + wred[1][1][j]) + (wred[1][2][j] + wred[1][3][j])) +
+                        ((wred[1][4][j] + wred[1][5][j]) + (wred[1][6][j] + wred[1][7][j]));
+        const float rinv = 1.0f / s;
+        for (int t = tid; t < Tq; t += AT_THREADS) {
+          const float al = es[t * KPB + j] * rinv;
+          es[t * KPB + j] = al;
+          if (align && t < Tp) align[(size_t)t * R + row0 + j] = al;
+        }
+      }
+  } else if (wv < nk) {
+    const int j = wv;
+    const int gs = KPB * Tq;
     float m = -INFINITY;
-    if (j < nk)
-#pragma unroll
-      for (int w = 0; w < AT_WAVES; ++w) m = fmaxf(m, wred[0][w][j]);
-    rmax[j] = m;
-    lsum[j] = 0.f;
-  }
-  // 3. softmax over t (torch: exp(x - max), sum, then * 1/sum)
-#pragma unroll
-  for (int j = 0; j < KPB; ++j)
-    if (j < nk)
-      for (int t = tid; t < Tq; t += AT_THREADS) {
-        const float p = expf(es[t * KPB + j] - rmax[j]);
-        es[t * KPB + j] = p;
-        lsum[j] += p;
+    for (int t = ln; t < Tq; t += 64) {
+      float ev = -INFINITY;
+      if (t < len) {
+        const float* x = xs + j * Tq + t;
+        ev = x[0];
+        for (int gg = 1; gg < G; ++gg) ev += x[gg * gs];
       }
-#pragma unroll
-  for (int j = 0; j < KPB; ++j)
-    if (j < nk) {
-      const float s = wave_sum(lsum[j]);
-      if (ln == 0) wred[1][wv][j] = s;
+      es[t * KPB + j] = ev;
+      m = fmaxf(m, ev);
     }
-  __syncthreads();
-  float rinv[KPB];
-#pragma unroll
-  for (int j = 0; j < KPB; ++j) {
+    m = wave_max(m);
     float s = 0.f;
-    if (j < nk)
-      s = ((wred[1][0][j] + wred[1][1][j]) + (wred[1][2][j] + wred[1][3][j])) +
-          ((wred[1][4][j] + wred[1][5][j]) + (wred[1][6][j] + wred[1][7][j]));
-    rinv[j] = 1.0f / s;
+    for (int t = ln; t < Tq; t += 64) {
+      const float p = expf(es[t * KPB + j] - m);
+      es[t * KPB + j] = p;
+      s += p;
+    }
+    const float rinv = 1.0f / wave_sum(s);
+    for (int t = ln; t < Tq; t += 64) {
+      const float al = es[t * KPB + j] * rinv;
+      es[t * KPB + j] = al;
+      if (align && t < Tp) align[(size_t)t * R + row0 + j] = al;
+    }
   }
-  const size_t RR = (size_t)R;
-#pragma unroll
-  for (int j = 0; j < KPB; ++j)
-    if (j < nk)
-      for (int t = tid; t < Tq; t += AT_THREADS) {
-        const float al = es[t * KPB + j] * rinv[j];
-        es[t * KPB + j] = al;
-        if (align && t < Tp) align[(size_t)t * RR + row0 + j] = al;
-      }
   __syncthreads();
 
   // 4. context: thread = 4 columns x every 4th t (4 partials, combined in a fixed order); 32
@@ -364,7 +470,7 @@ static size_t attn_lds_budget() { return (size_t)156 * 1024; }
 
 template <int KPB>
 static int attn_npf(int Tp) {
-  const size_t fixed = attn_smem_floats<KPB>(Tp) * sizeof(float) + 2 * AT_WAVES * KPB * sizeof(float);
+  const size_t fixed = attn_smem_floats<KPB>(Tp) * sizeof(float);
   const size_t budget = attn_lds_budget();
   const size_t room = fixed < budget ? budget - fixed : 0;
   const int rows = (int)(room / (C * sizeof(float))) & ~3;
@@ -384,8 +490,10 @@ static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart,
     raised = shm;
   }
   dim3 grid(a.B, (a.k + KPB - 1) / KPB);
-  hipLaunchKernelGGL(attention_kernel<KPB>, grid, dim3(AT_THREADS), shm, s, st, qpart, a.keysT, a.enc, a.lens,
-                     a.W + a.L.v, a.B * a.k, a.k, a.Tp, align, newdone, l, total, npf);
+  const float* ekT = a.keysT + (size_t)a.B * A * attn_tq(a.Tp);  // KeysEpi: [keys | exp(2 keys)]
+  hipLaunchKernelGGL(attention_kernel<KPB>, grid, dim3(AT_THREADS), shm, s, st, qpart, a.keysT, ekT, a.enc, a.lens,
+                     a.W + a.L.v, a.B * a.k, a.k, a.Tp, align, newdone, l, total, npf, a.attn_direct,
+                     dec_q_slots(a.B * a.k));
   return hipGetLastError();
 }
 

@@ -172,6 +172,7 @@ struct casr_handle {
   bool use_persistent = true;
   int precision = CASR_PREC_S16X3;  // requested (casr_set_precision)
   bool s16_valid = false;           // the bound blob's s16 images are usable (Layout::info)
+  bool proj_small = false;          // every |W_p| < 16 (Layout::info + 4)
   DevBuf x16;                       // s16 row image of the current layer input [B*Tp][Kp]
   bool s16() const { return precision == CASR_PREC_S16X3 && s16_valid; }
   int B = 0, Tp = 0;
@@ -334,6 +335,9 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
   if (w->attn_w_enc && !in_range(w->attn_w_enc, (size_t)C * A)) s16_ok = false;
   std::memset(out, 0, L.total * sizeof(float));
   out[L.info] = s16_ok ? 1.f : 0.f;
+  // info word 4: every projection weight below 16 in magnitude, so w_hi 2^11 is an f16 and the
+  // beam projection can run its one-accumulator s16x3 form (decoder.hip dgemm_kernel ONE)
+  out[L.info + 4] = (w->proj_w && in_range(w->proj_w, (size_t)cfg->vocab * KPROJ, 16.f)) ? 1.f : 0.f;
   // layout stamp: casr_bind_weights refuses a blob packed by a build with another layout
   const uint32_t stamp[3] = {LAYOUT_MAGIC, (uint32_t)(L.total & 0xFFFFFFFFu), (uint32_t)(L.total >> 32)};
   std::memcpy(out + L.info + 1, stamp, sizeof stamp);
@@ -428,7 +432,7 @@ int casr_create(const casr_config* cfg, int device, casr_handle** out) {
 int casr_bind_weights(casr_handle* h, const float* packed_device) {
   if (!h || !packed_device) return fail(h, CASR_ERR_ARG, "handle/weights NULL");
   HIP_OK(h, hipSetDevice(h->device));
-  float info[4] = {};
+  float info[5] = {};
   HIP_OK(h, hipMemcpy(info, packed_device + h->L.info, sizeof info, hipMemcpyDeviceToHost));
   uint32_t stamp[3];
   std::memcpy(stamp, info + 1, sizeof stamp);
@@ -438,6 +442,7 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
                 "casr_bind_weights: the blob was not packed by this build's layout (stamp %08x, %u floats; "
                 "expected %08x, %zu floats)", stamp[0], stamp[1], LAYOUT_MAGIC, h->L.total);
   h->s16_valid = info[0] == 1.f;
+  h->proj_small = info[4] == 1.f;
   h->W = packed_device;
   h->graphs.clear();  // captured graphs bake in the precision and weight pointers
   return CASR_OK;
@@ -501,8 +506,8 @@ int casr_recurrence_mode(const casr_handle* h, int B) {
 int casr_set_option(casr_handle* h, int option, int value) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
-  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0};
-  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8};
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8, 1};
   if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
     return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
   if (value < lo[option] || value > hi[option])
@@ -585,7 +590,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
   HIP_OK(h, h->cst.ensure((size_t)2 * B * H * sizeof(float)));
   HIP_OK(h, h->hfin.ensure((size_t)2 * B * H * sizeof(float)));
   const int Tq = (Tp + 3) & ~3;  // keysT row stride (16 B aligned rows for the attention)
-  HIP_OK(h, h->keysT.ensure((size_t)B * A * Tq * sizeof(float)));
+  HIP_OK(h, h->keysT.ensure(2 * (size_t)B * A * Tq * sizeof(float)));  // [keys | exp(2 keys)] (KeysEpi)
   HIP_OK(h, h->lens.ensure((size_t)B * sizeof(int32_t)));
   if (!fb) HIP_OK(h, hipMemcpyAsync(h->lens.p, lens, sizeof(int32_t) * B, hipMemcpyDeviceToDevice, s));
   const int layout = rec_layout(B, h->tune);
@@ -820,7 +825,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   const size_t smem = attention_smem_bytes(B, k, Tp, h->tune[CASR_OPT_ATTN_KPB]);
   if (smem > 160 * 1024)
     return fail(h, CASR_ERR_UNSUPPORTED, "attention needs %zu B of LDS (k=%d, Tp=%d) > 160 KiB", smem, k, Tp);
-  HIP_OK(h, h->st.ensure(((size_t)2 * R * ST + (size_t)(HD / 16) * R * A) * sizeof(float)));
+  HIP_OK(h, h->st.ensure(((size_t)2 * R * ST + (size_t)dec_q_slots(R) * R * A) * sizeof(float)));
   HIP_OK(h, h->logits.ensure(((size_t)R * V + (size_t)3 * R * GP_NB + (size_t)R * GP_NT) * sizeof(float)));
   HIP_OK(h, h->small.ensure((size_t)(6 * R + L + B + R + 1) * sizeof(int32_t) + 256));
   HIP_OK(h, h->bp.ensure((size_t)L * R * sizeof(int32_t)));
@@ -871,6 +876,8 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   a.prof = &h->prof;
   a.fuse_select = h->tune[CASR_OPT_FUSE_SELECT];
   a.attn_kpb = h->tune[CASR_OPT_ATTN_KPB];
+  a.attn_direct = h->tune[CASR_OPT_ATTN_DIRECT];
+  a.proj_small = h->proj_small;
   return CASR_OK;
 }
 
@@ -883,7 +890,9 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   if (!decode_graph_ok(h)) {
+    dg_trace_init();  // CASR_DG_TRACE diagnostics only
     HIP_OK(h, run_greedy(a, h->d, tokens, out_len, finished, accum, align, s));
+    dg_trace_dump();
     return CASR_OK;
   }
   // graph replay into handle-owned outputs, then copies to the caller's buffers
@@ -896,7 +905,7 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   float* ial = align ? iacc + B : nullptr;
   uint8_t* ifin = reinterpret_cast<uint8_t*>(iacc + B + nal);
   a.prof = nullptr;
-  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
+  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
                                      (uint64_t)(align != nullptr), (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->enc_out, (uint64_t)h->keysT.p,
                                      (uint64_t)h->hfin.p, (uint64_t)h->cst.p, (uint64_t)h->lens.p};
@@ -925,7 +934,9 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
   h->dec_k = k;
   h->beam_done = true;
   if (!decode_graph_ok(h)) {
+    dg_trace_init();  // CASR_DG_TRACE diagnostics only
     HIP_OK(h, run_beam(a, h->d, lm_weight, length_weight, best_tokens, best_len, best_score, steps, s));
+    dg_trace_dump();
     return CASR_OK;
   }
   const int B = h->B, L = h->cfg.max_len;
@@ -938,7 +949,7 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
   uint32_t lmw, lw;
   std::memcpy(&lmw, &lm_weight, 4);
   std::memcpy(&lw, &length_weight, 4);
-  const std::vector<uint64_t> key = {3, (uint64_t)a.s16, (uint64_t)a.attn_kpb, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
+  const std::vector<uint64_t> key = {3, (uint64_t)a.s16, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
                                      (uint64_t)h->gout.p, (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->bp.p, (uint64_t)h->tk.p, (uint64_t)h->rec.p,
                                      (uint64_t)h->enc_out, (uint64_t)h->keysT.p, (uint64_t)h->hfin.p,

@@ -139,6 +139,13 @@ CASR_DEV int row16_isum(int v) {
   return v + dpp_i<DPP_ROR8>(v);
 }
 
+// exp(2x) for the attention's split exponential score form (attention.hip): v_exp_f32 of
+// x * 2 log2(e) while |x| < 43 (a finite normal float), NaN beyond (the block then falls back to
+// the direct tanh(k + q) form)
+CASR_DEV float split_exp2x(float x) {
+  return fabsf(x) < 43.f ? __builtin_amdgcn_exp2f(x * 2.8853900817779268f) : __builtin_nanf("");
+}
+
 CASR_DEV float wave_max(float v) {
   v = row16_max(v);
   return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));

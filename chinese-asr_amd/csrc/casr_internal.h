@@ -68,9 +68,10 @@ struct Layout {
 
 Layout make_layout(const casr_config& cfg);
 
-// Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same bits.
+// Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
+// bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0, 0};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -265,7 +266,7 @@ struct DecodeBufs {
   float* st[2];          // [R][ST]
   float* logits;         // [R][V]
   GreedyPart part;       // per-block row partials of the projection (after the logits)
-  float* qpart;          // [HD/16][R][A] attention query partials, one per 16-unit block of h
+  float* qpart;          // [dec_q_slots(R)][R][A] attention query partials, one per LSTMCell column block
   int32_t* tok[2];       // [R]
   int32_t* src[2];       // [R]
   float* score[2];       // [R]
@@ -297,9 +298,14 @@ struct DecodeArgs {
   int greedy_run;        // set by run_greedy: the projection writes per-block argmax partials
   int fuse_select;       // CASR_OPT_FUSE_SELECT
   int attn_kpb;          // CASR_OPT_ATTN_KPB (0 auto)
+  int attn_direct;       // CASR_OPT_ATTN_DIRECT
+  int proj_small;        // every |W_p| < 16 (blob info word 4): the one-accumulator s16x3 projection
 };
 
 // attention.hip: one decode step's additive attention for all R rows (writes ctx into st)
+// attention query partials per decoder row: one per LSTMCell column block (decoder.hip
+// launch_dec_lstm), 16 units each at R <= 512, 32 units at R > 512
+inline int dec_q_slots(int R) { return R > 512 ? HD / 32 : HD / 16; }
 hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
                                  int32_t* newdone, int l, int total, hipStream_t s);
 size_t attention_smem_bytes(int B, int k, int Tp, int opt);

@@ -110,16 +110,32 @@ __device__ __forceinline__ void static_for(F&& f) {
 // LDS feeds RS MFMA rows) by NT / WC of the block's column tiles; KQ = 8 / (WR WC) k slices.
 // IL (s16): the next tile's DMA slots are issued between this tile's MFMA groups (one per column
 // tile of the wave's first k-step) instead of in one burst after the barrier.
-template <int WR, int NT, int S, class ASrc, class Epi, bool S16 = false, int RS = 1, int WC = 1, bool IL = false>
+// BKW = 32 (s16 only): each ring stage holds ONE 32-deep k-step instead of a 64-deep tile, so the
+// same LDS carries twice the rows or columns (the 256 x 160 beam projection block) or twice the
+// stages in flight.  Stage kt is k-step js = kt of the 64-deep form: the same wave (kq = kt % KQ)
+// multiplies the same operands in the same order, so both forms give the same bits.  A stage of
+// a row is its 8 16-B pieces of words 64 (kt >> 1) + 16 p' + 8 (kt & 1) + {0, 4} (p = 2 p' + {0,1}),
+// piece p stored at slot p ^ (row & 7); the W stage is half j = kt & 1 of the fragment block.
+// ONE (s16, weights |w| < 16: blob info word 4): one accumulator per tile carrying the whole s16x3
+// sum scaled by 2^11, acc += a_hi (w_hi 2^11) + a_hi w_lo' + a_lo' w_hi (w_hi 2^11 formed by one
+// v_pk_mul_f16, exact while |w| < 32), as the encoder's input projection (gemm16.hip): half the
+// accumulator registers of the (hi.hi, cross) pair, which the 256 x 160 block cannot hold.
+template <int WR, int NT, int S, class ASrc, class Epi, bool S16 = false, int RS = 1, int WC = 1, bool IL = false,
+          int BKW = 64, bool ONE = false>
 __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntiles, int nkt,
                                                     const float* __restrict__ Wf, ASrc asrc, Epi epi) {
   constexpr int KQ = 8 / (WR * WC), QPW = 4 / KQ, BM = 16 * WR * RS, NTW = NT / WC;
-  static_assert(128 % BM == 0, "row blocks tile the fused select's 128 token slots");
   static_assert(WR * WC * KQ == 8 && NT % WC == 0 && KQ <= 4, "8 waves = row groups x column groups x k slices");
-  constexpr int ATILE = BM * DG_BK, WTILE = NT * FRAG;
+  constexpr bool B32 = BKW == 32;
+  static_assert(BKW == 64 || (B32 && S16), "32-deep stages: s16 images only");
+  static_assert(!ONE || S16, "one accumulator: s16 images only");
+  constexpr int WFR = B32 ? FRAG / 2 : FRAG;       // W floats of one column tile per stage
+  constexpr int RPI = B32 ? 8 : 4, WPI = B32 ? 2 : 4;  // A rows / W DMA instructions per 1 KB DMA
+  constexpr int ATILE = BM * BKW, WTILE = NT * WFR;
   constexpr int STG = ATILE + WTILE;          // floats per stage: [A tile | W tile]
-  constexpr int NA = BM / 4, NDMA = NA + 4 * NT;  // DMA instructions per stage: A (4 rows each) + W
+  constexpr int NA = BM / RPI, NDMA = NA + WPI * NT;  // DMA instructions per stage: A + W
   constexpr int NSLOT = (NDMA + 7) / 8;      // per wave (at most)
+  const int nkb = B32 ? nkt / 2 : nkt;        // 64-deep fragment blocks per W column tile
   static_assert(S >= 2 && S <= 6, "ring of 2..6 stage buffers");
   static_assert(S * STG * 4 <= 160 * 1024, "ring fits the LDS");
   static_assert((S - 2) * NSLOT < 64, "vmcnt range");
@@ -153,19 +169,28 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   asrc.template prologue<BM>(rb * BM, nb == 0);
   // per-lane DMA sources that do not depend on k: A row segment bases, W fragment block bases
   int bad = 0;
-  const float* aseg[NSLOT][2];
-  const float* wsrc[NSLOT];
+  // (a source with one segment (kSeg == 0) keeps one pointer per slot; W sources are 32-bit
+  // offsets from Wf: registers the 256 x 160 block needs for its accumulators)
+  constexpr int NSEG = ASrc::kSeg > 0 ? 2 : 1;
+  const float* aseg[NSLOT][NSEG];
+  uint32_t woff[NSLOT];
 #pragma unroll
   for (int j = 0; j < NSLOT; ++j) {
     const int i = w + 8 * j;
-    aseg[j][0] = aseg[j][1] = wsrc[j] = nullptr;
+    woff[j] = 0;
+#pragma unroll
+    for (int q = 0; q < NSEG; ++q) aseg[j][q] = nullptr;
     if (i < NA) {
-      asrc.bind(rb * BM + 4 * i + (lane >> 4), aseg[j][0], aseg[j][1], bad);
+      const float* s0;
+      const float* s1;
+      asrc.bind(rb * BM + RPI * i + lane / (64 / RPI), s0, s1, bad);
+      aseg[j][0] = s0;
+      aseg[j][NSEG - 1] = s1;
     } else if (i < NDMA) {
-      const int tn = (i - NA) >> 2, qq = (i - NA) & 3;
+      const int tn = (i - NA) / WPI, qq = (i - NA) % WPI;
       int t = nb * NT + tn;
       t = t < ntiles ? t : ntiles - 1;
-      wsrc[j] = Wf + (size_t)t * nkt * FRAG + qq * 256 + lane * 4;
+      woff[j] = (uint32_t)(t * nkb * FRAG + qq * 256 + lane * 4);
     }
   }
   auto stage_slot = [&](float* dst, int kt, auto J) {
@@ -173,50 +198,75 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
     if constexpr (j < NSLOT) {
       float* la = dst;
       float* lw = dst + ATILE;
-      const int k0 = kt * DG_BK;
+      const int kb = B32 ? kt >> 1 : kt, k0 = kb * 64;
       const int i = w + 8 * j;
       if (i < NA) {
-        const int row = 4 * i + (lane >> 4), c = (lane & 15) ^ (row & 15);
-        const float* src = k0 < ASrc::kSeg ? aseg[j][0] + k0 : aseg[j][1] + (k0 - ASrc::kSeg);
-        lds_dma16(src + c * 4, la + i * 256);
+        const float* seg = k0 < ASrc::kSeg ? aseg[j][0] + k0 : aseg[j][NSEG - 1] + (k0 - ASrc::kSeg);
+        if constexpr (B32) {
+          const int row = 8 * i + (lane >> 3), p = (lane & 7) ^ (row & 7);
+          lds_dma16(seg + 16 * (p >> 1) + 8 * (kt & 1) + 4 * (p & 1), la + i * 256);
+        } else {
+          const int row = 4 * i + (lane >> 4), c = (lane & 15) ^ (row & 15);
+          lds_dma16(seg + c * 4, la + i * 256);
+        }
       } else if (i < NDMA) {
-        const int tn = (i - NA) >> 2, qq = (i - NA) & 3;
-        lds_dma16(wsrc[j] + (size_t)kt * FRAG, lw + tn * FRAG + qq * 256);
+        const int tn = (i - NA) / WPI, qq = (i - NA) % WPI;
+        lds_dma16(Wf + woff[j] + (size_t)kb * FRAG + (B32 ? (kt & 1) * 512 : 0), lw + tn * WFR + qq * 256);
       }
     }
   };
   auto stage = [&](float* dst, int kt) { static_for<0, NSLOT>([&](auto J) { stage_slot(dst, kt, J); }); };
   constexpr bool ILS = IL && S16;
 
-  f32x4 acc[RS][NTW], accx[RS][NTW];
+  f32x4 acc[RS][NTW], accx[ONE ? 1 : RS][ONE ? 1 : NTW];
 #pragma unroll
   for (int rs = 0; rs < RS; ++rs)
 #pragma unroll
-    for (int tn = 0; tn < NTW; ++tn) acc[rs][tn] = accx[rs][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int tn = 0; tn < NTW; ++tn) {
+      acc[rs][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (!ONE) accx[rs][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   auto arow = [&](int rs) { return (ws * RS + rs) * 16 + r; };
   auto compute = [&](const float* src, int kt, auto&& issue) {
     const float* la = src;
-    const float* lw = src + ATILE + wc * NTW * FRAG;
+    const float* lw = src + ATILE + wc * NTW * WFR;
     if constexpr (S16) {
       bool pend = ILS;  // DMA slots of the next tile not issued yet (wave-uniform)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if ((2 * kt + j) % KQ != kq) continue;
-        const int c0 = 4 * g + 2 * j;
+      for (int j = 0; j < (B32 ? 1 : 2); ++j) {
+        if ((B32 ? kt : 2 * kt + j) % KQ != kq) continue;
         f16x8 ah[RS], al[RS];
 #pragma unroll
         for (int rs = 0; rs < RS; ++rs) {
           const int ar = arow(rs);
-          const u32x4 w0 = *reinterpret_cast<const u32x4*>(la + ar * DG_BK + ((c0 ^ (ar & 15)) << 2));
-          const u32x4 w1 = *reinterpret_cast<const u32x4*>(la + ar * DG_BK + (((c0 + 1) ^ (ar & 15)) << 2));
+          u32x4 w0, w1;
+          if constexpr (B32) {  // pieces 2g, 2g + 1 of the row's stage
+            w0 = *reinterpret_cast<const u32x4*>(la + ar * 32 + (((2 * g) ^ (ar & 7)) << 2));
+            w1 = *reinterpret_cast<const u32x4*>(la + ar * 32 + (((2 * g + 1) ^ (ar & 7)) << 2));
+          } else {
+            const int c0 = 4 * g + 2 * j;
+            w0 = *reinterpret_cast<const u32x4*>(la + ar * DG_BK + ((c0 ^ (ar & 15)) << 2));
+            w1 = *reinterpret_cast<const u32x4*>(la + ar * DG_BK + (((c0 + 1) ^ (ar & 15)) << 2));
+          }
           unpack16(w0, w1, ah[rs], al[rs]);
         }
         static_for<0, NTW>([&](auto TN) {
           constexpr int tn = decltype(TN)::value;
-          const f16x8 bh = *reinterpret_cast<const f16x8*>(lw + tn * FRAG + (2 * j) * 256 + lane * 4);
-          const f16x8 bl = *reinterpret_cast<const f16x8*>(lw + tn * FRAG + (2 * j + 1) * 256 + lane * 4);
+          const int jw = B32 ? 0 : 2 * j;  // the stage's W half: [hi | lo][lane][8 halves]
+          const f16x8 bh = *reinterpret_cast<const f16x8*>(lw + tn * WFR + jw * 256 + lane * 4);
+          const f16x8 bl = *reinterpret_cast<const f16x8*>(lw + tn * WFR + (jw + 1) * 256 + lane * 4);
+          if constexpr (ONE) {
+            const f16x8 b1 = bh * (_Float16)2048.0f;
 #pragma unroll
-          for (int rs = 0; rs < RS; ++rs) mfma_s16(ah[rs], al[rs], bh, bl, acc[rs][tn], accx[rs][tn]);
+            for (int rs = 0; rs < RS; ++rs) {
+              acc[rs][tn] = mfma16x16x32h(ah[rs], b1, acc[rs][tn]);
+              acc[rs][tn] = mfma16x16x32h(ah[rs], bl, acc[rs][tn]);
+              acc[rs][tn] = mfma16x16x32h(al[rs], bh, acc[rs][tn]);
+            }
+          } else {
+#pragma unroll
+            for (int rs = 0; rs < RS; ++rs) mfma_s16(ah[rs], al[rs], bh, bl, acc[rs][tn], accx[rs][tn]);
+          }
           if constexpr (ILS) {
             if (pend) issue(TN);
           }
@@ -295,14 +345,17 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   stamp(3);
   if (kq == 0)
 #pragma unroll
-    for (int rs = 0; rs < RS; ++rs) epi.late(pre[rs], erow0(rs), nbw, lane & 15);  // under the k-slice exchange
+    for (int rs = 0; rs < RS; ++rs) epi.template late<NTW>(pre[rs], erow0(rs), nbw, lane & 15);  // under the k-slice exchange
   if constexpr (S16) {
 #pragma unroll
     for (int rs = 0; rs < RS; ++rs)
 #pragma unroll
       for (int tn = 0; tn < NTW; ++tn)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[rs][tn][e] = s16_combine(acc[rs][tn][e], accx[rs][tn][e]);
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (ONE) acc[rs][tn][e] *= S16_LO_INV;
+          else acc[rs][tn][e] = s16_combine(acc[rs][tn][e], accx[rs][tn][e]);
+        }
   }
   // k slices 1..KQ-1 hand their partial sums to slice 0 through LDS (the ring is free now)
   if constexpr (KQ > 1) {
@@ -335,7 +388,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   // per-wave LDS scratch for the epilogue (ring buffers are free now; the k-slice exchange
   // above used lb0 (only when KQ > 1, i.e. at most 4 epilogue waves, all on lb1)): 16 rows x
   // (16 NTW + 4) floats per epilogue wave, reused by its RS slabs in turn (LDS is in order per wave)
-  static_assert(4 * 16 * (16 * NTW + 4) <= STG, "epilogue slabs fit a stage buffer");
+  static_assert(!Epi::kScratch || 4 * 16 * (16 * NTW + 4) <= STG, "epilogue slabs fit a stage buffer");
   const int ew = ws * WC + wc;
   float* escr = (ew < 4 ? lb1 : lb0) + (ew & 3) * 16 * (16 * NTW + 4);
 #pragma unroll
@@ -343,17 +396,23 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   stamp(4);
 }
 
-template <int WR, int NT, int S, int RS = 1, int WC = 1, bool IL = false, class ASrc, class Epi>
+template <int WR, int NT, int S, int RS = 1, int WC = 1, bool IL = false, int BKW = 64, bool ONE = false, class ASrc,
+          class Epi>
 static void launch_dg(int NB, int R, int ntiles, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi,
                       int s16, hipStream_t s) {
   constexpr int BM = 16 * WR * RS;
   const int NR = (R + BM - 1) / BM;
-  if (s16)
-    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s,
-                       NB, NR, ntiles, nkt, Wf, asrc, epi);
-  else
-    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, false, RS, WC>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s,
-                       NB, NR, ntiles, nkt, Wf, asrc, epi);
+  if constexpr (BKW == 32 || ONE) {  // s16 only (the f32 form of the same shape does not fit the LDS)
+    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL, BKW, ONE>), dim3(xcd_grid(NB, NR)),
+                       dim3(512), 0, s, NB, NR, ntiles, nkt * (64 / BKW), Wf, asrc, epi);
+  } else {
+    if (s16)
+      hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL>), dim3(xcd_grid(NB, NR)), dim3(512), 0,
+                         s, NB, NR, ntiles, nkt, Wf, asrc, epi);
+    else
+      hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, false, RS, WC>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s,
+                         NB, NR, ntiles, nkt, Wf, asrc, epi);
+  }
 }
 
 // A rows of the decoder LSTM: [embed(tok[r]) | st_old[src[r]][0:1024] = ctx | h]; a 64-deep
@@ -395,6 +454,7 @@ struct DecLstmA {
   // issued before the first reduction: one round trip for the block, not one per row
   template <int BM>
   __device__ __forceinline__ void prologue(int row0, bool writer) const {
+    static_assert(128 % BM == 0, "row blocks tile the fused select's 128 token slots");
     if (!sel) return;
     constexpr int RPW = BM / 8;  // rows per wave
     int* st = sel_tok_lds();
@@ -477,74 +537,98 @@ struct DecLstmA {
 
 struct DecLstmEpi {
   static constexpr int kTraceClass = 0;
+  static constexpr bool kScratch = false;  // the epilogue's LDS: its own h tiles (ht), no slab
   const float* bias;  // packed [4HD]
   const float* st_old;
   float* st_new;
   DecLstmA rows;      // guarded predecessor lookup
   const int32_t* newdone;
   const float* w_hidden;  // [HD][A]
-  float* qpart;           // [HD/16][R][A]
+  float* qpart;           // [dec_q_slots(R)][R][A]
   int R, l, total;
   int hw = 0;  // s16x3 arithmetic: the hardware-exp cell (casr_common.h lstm_cell_hw, as the encoder's)
   // operands loaded before the k loop: gate biases, predecessor rows, this lane's W_hidden
-  // fragments of the query partial (A/16 x 4 MFMA steps); c of the predecessor after it
+  // fragments of the query partial (A/16 x 4 MFMA steps); c of the predecessor after it.  A block
+  // of NTN = 4 UG column tiles holds UG 16-unit groups (4 gate tiles each): [i f g o] of units
+  // 16 (nb UG + ug) ..+15 (the packed gate-row order)
+  static constexpr int UGMAX = 2;
   struct Pre {
-    float bg[4];
+    float bg[UGMAX][4];
     int srow[4];
-    float wh[A / 16][4];
-    float cold[4];
+    float wh[UGMAX][A / 16][4];
+    float cold[UGMAX][4];
   };
   __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
   __device__ __forceinline__ int32_t* err_flags() const { return rows.err; }
   template <int NTN>
   __device__ __forceinline__ void prefetch(Pre& p, int row0, int nb, int u, int& bad) const {
+    constexpr int UG = NTN / 4;
     const int lane = threadIdx.x & 63, g = lane >> 4;
 #pragma unroll
-    for (int gt = 0; gt < 4; ++gt) p.bg[gt] = bias[nb * 64 + gt * 16 + u];
+    for (int ug = 0; ug < UG; ++ug)
+#pragma unroll
+      for (int gt = 0; gt < 4; ++gt) p.bg[ug][gt] = bias[(nb * UG + ug) * 64 + gt * 16 + u];
 #pragma unroll
     for (int e = 0; e < 4; ++e) p.srow[e] = rows.safe_src(min(row0 + e, R - 1), bad);
-    const float* wp = w_hidden + (size_t)(nb * 16 + g) * A + (lane & 15);
 #pragma unroll
-    for (int at = 0; at < A / 16; ++at)
+    for (int ug = 0; ug < UG; ++ug) {
+      const float* wp = w_hidden + (size_t)((nb * UG + ug) * 16 + g) * A + (lane & 15);
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) p.wh[at][kk] = wp[(size_t)(4 * kk) * A + at * 16];
+      for (int at = 0; at < A / 16; ++at)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) p.wh[ug][at][kk] = wp[(size_t)(4 * kk) * A + at * 16];
+    }
   }
+  template <int NTN = 4>
   __device__ __forceinline__ void late(Pre& p, int row0, int nb, int u) const {
-    const int U = nb * 16 + u;
+    constexpr int UG = NTN / 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) p.cold[e] = st_old[(size_t)p.srow[e] * ST + C + HD + U];
+    for (int ug = 0; ug < UG; ++ug) {
+      const int U = (nb * UG + ug) * 16 + u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) p.cold[ug][e] = st_old[(size_t)p.srow[e] * ST + C + HD + U];
+    }
   }
   template <int NTN = 4>
   __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p, float*) const {
-    static_assert(NTN == 4, "the LSTM cell needs the 4 gate tiles of a 64-column block");
-    __shared__ float ht[8][16][17];  // per row-slab wave (<= 8 per block): h tile [row][unit]
+    static_assert(NTN % 4 == 0 && NTN / 4 <= UGMAX, "the LSTM cell needs the 4 gate tiles of each 16-unit group");
+    constexpr int UG = NTN / 4;
+    // per row-slab wave (<= 8 per block): the h tile [row][unit] of its UG unit groups; the query
+    // partial of the block's 16 UG units is one MFMA chain over them (qpart slot nb, dec_q_slots)
+    __shared__ float ht[8][16][16 * UGMAX + 1];
     const int lane = threadIdx.x & 63, ws = (row0 >> 4) & 7, g = lane >> 4;
-    const int U = nb * 16 + u;
+    const int rbase = row0 - 4 * g;  // first row of this wave's slab
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = row0 + e;
-      float h2 = 0.f, c2;
-      if (row < R) {
-        if (hw)  // performance arithmetic (~1e-7 absolute, like the encoder's s16x3 cell)
-          lstm_cell_hw(acc[0][e] + p.bg[0], acc[1][e] + p.bg[1], acc[2][e] + p.bg[2], acc[3][e] + p.bg[3], p.cold[e],
-                       h2, c2);
-        else  // f32 arithmetic: libm cell, torch's CPU formulas
-          lstm_cell(acc[0][e] + p.bg[0], acc[1][e] + p.bg[1], acc[2][e] + p.bg[2], acc[3][e] + p.bg[3], p.cold[e], h2,
-                    c2);
-        st_new[(size_t)row * ST + C + U] = h2;
-        st_new[(size_t)row * ST + C + HD + U] = c2;
-        reinterpret_cast<uint32_t*>(st_new)[(size_t)row * ST + ST16 + C + U] = split16_word(h2);
+    for (int ug = 0; ug < UG; ++ug) {
+      const int U = (nb * UG + ug) * 16 + u;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = row0 + e;
+        float h2 = 0.f, c2;
+        if (row < R) {
+          const f32x4* ag = acc + 4 * ug;
+          if (hw)  // performance arithmetic (~1e-7 absolute, like the encoder's s16x3 cell)
+            lstm_cell_hw(ag[0][e] + p.bg[ug][0], ag[1][e] + p.bg[ug][1], ag[2][e] + p.bg[ug][2],
+                         ag[3][e] + p.bg[ug][3], p.cold[ug][e], h2, c2);
+          else  // f32 arithmetic: libm cell, torch's CPU formulas
+            lstm_cell(ag[0][e] + p.bg[ug][0], ag[1][e] + p.bg[ug][1], ag[2][e] + p.bg[ug][2], ag[3][e] + p.bg[ug][3],
+                      p.cold[ug][e], h2, c2);
+          st_new[(size_t)row * ST + C + U] = h2;
+          st_new[(size_t)row * ST + C + HD + U] = c2;
+          reinterpret_cast<uint32_t*>(st_new)[(size_t)row * ST + ST16 + C + U] = split16_word(h2);
+        }
+        ht[ws][4 * g + e][16 * ug + u] = h2;
       }
-      ht[ws][4 * g + e][u] = h2;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the tile is read back by other lanes of this wave
     __builtin_amdgcn_wave_barrier();
-    const int rbase = row0 - 4 * g;  // first row of this wave's slab
 #pragma unroll
     for (int at = 0; at < A / 16; ++at) {
       f32x4 q = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) q = mfma16x16x4(ht[ws][lane & 15][4 * kk + g], p.wh[at][kk], q);
+      for (int ug = 0; ug < UG; ++ug)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) q = mfma16x16x4(ht[ws][lane & 15][16 * ug + 4 * kk + g], p.wh[ug][at][kk], q);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = rbase + 4 * g + e;
@@ -573,6 +657,7 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
 
 struct ProjEpi {
   static constexpr int kTraceClass = 1;
+  static constexpr bool kScratch = true;  // beam logits go out through per-wave LDS slabs
   const float* bias;
   float* logits;  // [R][V] (beam); nullptr in greedy mode
   // per-block row partials (greedy; beam at temperature 1 for its logsumexp and threshold), or
@@ -595,6 +680,7 @@ struct ProjEpi {
       p.bn[tn] = n < V ? bias[n] : 0.f;
     }
   }
+  template <int NTN>
   __device__ __forceinline__ void late(Pre&, int, int, int) const {}
   template <int NTN = 4>
   __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p,
@@ -1494,26 +1580,36 @@ static void launch_dec_lstm(int R, const float* Wf, const ASrc& asrc, const Epi&
   const int NB = HD / 16, ntiles = 4 * NB, nkt = KDEC / DG_BK;
   if (R <= 256) launch_dg<2, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 512) launch_dg<4, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  else launch_dg<8, 4, 3, 1, 1, true>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  // R > 512: 128 rows x 128 columns (two 16-unit groups): at R = 2048 one round of 256 blocks,
+  // 1.3 MB per block, instead of two rounds of 128 x 64 blocks (ring 3) at 0.98 MB each; s16: a
+  // ring of four 32-deep stages (three in flight), f32: two 64-deep stages
+  else if (!s16) launch_dg<8, 8, 2, 1, 1, true>(NB / 2, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else launch_dg<8, 8, 4, 1, 1, true, 32>(NB / 2, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
 template <class ASrc, class Epi>
-static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi, int s16,
+static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi, int s16, int small_w,
                         hipStream_t s) {
   const int nkt = KPROJ / DG_BK, NB = (ntiles + 4) / 5;  // 5 column tiles per block (10 at R > 512)
   // R <= 32 (BASELINE config 2): 32-row blocks, so no block stages and multiplies 32 padding rows
   if (R <= 32) launch_dg<2, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 256) launch_dg<4, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 512) launch_dg<8, 5, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  else launch_dg<4, 10, 2, 2, 2, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  else if (!s16 || !small_w) launch_dg<4, 10, 2, 2, 2, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  // s16 at R > 512 with |W_p| < 16: 256 x 160 blocks of 32-deep stages, ring 3, one accumulator
+  // (one round of 256 blocks at R = 2048, 1.7 MB per block, against two rounds of 128 x 160 blocks
+  // at 1.2 MB each)
+  else launch_dg<8, 10, 3, 2, 1, true, 32, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
 // ------------------------------------------------------------------ host drivers
 // per-block row partials from the projection epilogue: the vocabulary must fit the 64 partial
 // blocks; beam search uses them at temperature 1 only (they are of x, not x / T)
 static int proj_col_blocks(const DecodeArgs& a) {
-  const int nt = a.L.VP / 16;
-  return (nt + 4) / 5;  // 5-tile column blocks (at R > 512: two per 10-tile block, one per wave column)
+  const int nt = a.L.VP / 16, R = a.B * a.k;
+  // the column block of a wave (ProjEpi's partial index): 5 tiles, 10 for the one-accumulator
+  // 256 x 160 beam block (launch_proj: s16, R > 512, |W_p| < 16)
+  return a.s16 && a.proj_small && R > 512 ? (nt + 9) / 10 : (nt + 4) / 5;
 }
 static bool row_partials(const DecodeArgs& a) {
   return proj_col_blocks(a) <= GP_NB && (a.greedy_run || a.temperature == 1.0f);
@@ -1549,7 +1645,7 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
     GreedyPart gp = parts ? d.part : GreedyPart{nullptr, nullptr, nullptr, nullptr};
     if (a.greedy_run || a.V > 16 * GP_NT) gp.tmx = nullptr;  // tile maxima: beam only
     ProjEpi epi{a.W + a.L.proj_b, a.greedy_run && parts ? nullptr : d.logits, d.newdone, R, a.V, l, total, d.err, gp};
-    launch_proj(R, a.L.VP / 16, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, s);
+    launch_proj(R, a.L.VP / 16, a.W + (a.s16 ? a.L.proj_w16 : a.L.proj_w), asrc, epi, a.s16, a.proj_small, s);
   }
   return hipGetLastError();
 }

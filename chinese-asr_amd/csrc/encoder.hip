@@ -36,14 +36,20 @@ struct StoreBiasEpi {  // C[row][col] = acc + bias[col]; N % 4 == 0, rows 16 B a
   }
 };
 
-struct KeysEpi {  // keysT[b][a][t] = acc + b_attn[a], row = b*Tp + t, row stride Tq
+// keysT[b][a][t] = acc + b_attn[a], row = b*Tp + t, row stride Tq; and behind the B x A x Tq keys,
+// ekT = exp(2 keys) for the attention's split exponential score form (attention.hip split_exp2x:
+// v_exp_f32 of keys * 2 log2(e), NaN where |keys| >= 43, which sends a block to the direct form)
+struct KeysEpi {
   static constexpr bool kRowTile = false;
   float* keysT;
   const float* bias;
-  int Tp, Tq;
+  int Tp, Tq, B;
   __device__ __forceinline__ void operator()(int row, int col, float v) const {
     const int b = row / Tp, t = row - b * Tp;
-    keysT[((size_t)b * A + col) * Tq + t] = v + bias[col];
+    const float k = v + bias[col];
+    const size_t i = ((size_t)b * A + col) * Tq + t;
+    keysT[i] = k;
+    keysT[(size_t)B * A * Tq + i] = split_exp2x(k);
   }
 };
 
@@ -324,7 +330,7 @@ hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, cons
                        float* keysT, hipStream_t s) {
   const int M = B * Tp;
   if (M <= 0) return hipErrorInvalidValue;
-  KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3};
+  KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3, B};
   const TileOrder order = tile_order(A / GB_N, (M + GB_M - 1) / GB_M, C);
   hipLaunchKernelGGL(gemm_nt_kernel<KeysEpi>, dim3(order.blocks()), dim3(256), 0, s, enc, C, wencT,
                      C, M, A, C, order, epi);
@@ -337,7 +343,7 @@ hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc1
                            float* keysT, hipStream_t s) {
   const int M = B * Tp;
   if (M <= 0 || C % GB_K != 0) return hipErrorInvalidValue;
-  KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3};
+  KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3, B};
   const TileOrder order = tile_order(A / GB_N, (M + GB_M - 1) / GB_M, C);
   hipLaunchKernelGGL((gemm_nt_kernel<KeysEpi, true>), dim3(order.blocks()), dim3(256), 0, s, enc16, C, wenc16,
                      C, M, A, C, order, epi);

@@ -231,7 +231,12 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *   CASR_OPT_GEMM16_TAIL     1: the persistent kernel takes whole rounds of tiles, the rows after
  *                            them go to one launch of half tiles (default); 0: partial last round
  *   CASR_OPT_ATTN_KPB        beam rows per attention block at k > 2: 0 auto (8 at B >= 256 and
- *                            k >= 8, else 4), 4 or 8 */
+ *                            k >= 8, else 4), 4 or 8
+ * One option selects a numerics variant instead (results within the attention tolerance, not bit
+ * for bit; tests/test_gpu_parity.py compares the two):
+ *   CASR_OPT_ATTN_DIRECT     0: attention scores in the split exponential form 1 - 2 / (1 + e^{2k}
+ *                            e^{2q}) (default; one transcendental per term); 1: the
+ *                            direct tanh(k + q) form the split form falls back to per block */
 enum {
   CASR_OPT_FUSE_SELECT = 0,
   CASR_OPT_REC_LAYOUT = 1,
@@ -242,7 +247,8 @@ enum {
   CASR_OPT_GEMM16_PERSIST = 6,
   CASR_OPT_GEMM16_TAIL = 7,
   CASR_OPT_ATTN_KPB = 8,
-  CASR_OPT_COUNT = 9
+  CASR_OPT_ATTN_DIRECT = 9,
+  CASR_OPT_COUNT = 10
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

@@ -460,6 +460,47 @@ def test_keys_elementwise_match_oracle(eng, name):
         np.testing.assert_allclose(keys[b].T, ref, atol=2e-5, rtol=0)
 
 
+@pytest.mark.parametrize("name", ["plain", "peaked"])
+def test_attention_split_form_vs_direct(eng, name):
+    """The attention's split exponential score form (default: sum_a v_a - 2 v_a / (1 + e^{2k}
+    e^{2q}), attention.hip) against the direct tanh(k + q) form (CASR_OPT_ATTN_DIRECT), greedy and
+    beam 8: same tokens, greedy alignments within 1e-5 and scores within 2e-4.  Then a blob whose
+    attention bias puts every key above 43 (outside the split form's range, where e^{2k} is stored
+    as NaN): every block falls back to the direct form, so the two options agree bit for bit."""
+    def run():
+        g = eng.greedy(alignment=True)
+        bm = eng.beam(8)
+        assert eng.device_flags() == 0
+        return [x.cpu() for x in (g["tokens"], g["out_len"], g["accum"], g["alignment"], bm["tokens"],
+                                  bm["length"], bm["score"])]
+
+    def both():
+        split = run()
+        try:
+            eng.set_option("ATTN_DIRECT", 1)
+            direct = run()
+        finally:
+            eng.set_option("ATTN_DIRECT", 0)
+        return split, direct
+
+    bind(eng, name)
+    feat, flen = golden_features(eng)
+    eng.encode(feat, flen)
+    split, direct = both()
+    for i in (0, 1, 4, 5):
+        assert torch.equal(split[i], direct[i])
+    for i, tol in ((2, 2e-4), (3, 1e-5), (6, 2e-4)):
+        np.testing.assert_allclose(split[i].numpy(), direct[i].numpy(), atol=tol, rtol=0)
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=(name == "peaked"))
+    dec_sd = dict(dec_sd)
+    dec_sd["attn_mechanism.b_attn"] = dec_sd["attn_mechanism.b_attn"] + 50.0
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    eng.encode(feat, flen)
+    split, direct = both()
+    for a, b in zip(split, direct):
+        assert torch.equal(a, b)
+
+
 def test_bind_refuses_foreign_blob(eng):
     """A blob of another layout (size or stamp) is refused on bind, not read past its end."""
     from casr import lib as L

@@ -52,7 +52,8 @@ eng.encode(feat, flen)
 eng.greedy()["tokens"].cpu()
 eng.greedy()["tokens"].cpu()
 if os.environ.get("BEAM"):
-    eng.encode(feat[:128].contiguous(), flen[:128].contiguous())
+    BB = int(os.environ.get("BB", 128))
+    eng.encode(feat[:BB].contiguous(), flen[:BB].contiguous())
     kb = int(os.environ.get("K", 8))
     eng.beam(kb)["tokens"].cpu()
     eng.beam(kb)["tokens"].cpu()
