@@ -95,8 +95,8 @@ def kernel_bytes(cls, B, Tp, R, V):
         return 4.0 * B * Tp * (A + C)
     if cls == "dec_lstm":    # W image, the gathered A rows, new h / c / h16 and the query partials
         return 4.0 * (4 * HD * (E + C + HD) + R * (E + C + HD) + 3 * R * HD + (HD // 16) * R * A)
-    if cls == "proj":        # W image, [ctx | h] rows, per-block (max, sum, argmax) partials
-        return 4.0 * (VP * (C + HD) + R * (C + HD) + 3 * R * 64)
+    if cls == "proj":        # W image, [ctx | h] rows, per-block (max, sum, argmax) partials; beam: + logits
+        return 4.0 * (VP * (C + HD) + R * (C + HD) + 3 * R * 64 + (R * V + R * (VP // 16) if R > B else 0))
     return None
 
 
@@ -299,15 +299,15 @@ def main():
     Tp = T // 3
     value = B * world * args.steps / dt
     ms_step = 1000.0 * dt / args.steps
-    pmc = {}
-    pmc_file = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_file):
+    def load_pmc(name):
         try:
-            pmc = json.load(open(pmc_file))
+            return json.load(open(os.path.join(REPO, "profiles", name)))
         except Exception:
-            pmc = {}
+            return {}
+    # committed PMC passes (tools/probes/profile_r03.sh): greedy step, and beam 8 at B = 256
+    pmc_greedy, pmc_beam = load_pmc("pmc_traffic.json"), load_pmc("pmc_traffic_beam.json")
 
-    def roof(cls, launches, ms, steps, Bc, Rc):
+    def roof(cls, launches, ms, steps, Bc, Rc, pmc=pmc_greedy):
         """Achieved rate of one kernel class: algorithmic work of `steps` steps over its launches'
         summed duration, against the peak of its bound; PMC columns from the committed passes."""
         work, bound = kernel_work(cls, Bc, Tp, Rc, cfg.vocab, T)
@@ -360,7 +360,8 @@ def main():
                 "unit": "utt/s", "ms_per_step": 1000.0 * dtb / steps,
                 "rtf": dtb / steps / (Bb * world * AUDIO_S_PER_UTT),
                 "kernel_breakdown_ms": {c: round(v[1], 3) for c, v in bd.items()},
-                "kernels": {c: roof(c, n, ms, 1, Bb, Bb * k) for c, (n, ms) in bd.items()}}
+                "kernels": {c: roof(c, n, ms, 1, Bb, Bb * k, pmc_beam if Bb == 256 and k == 8 else {})
+                            for c, (n, ms) in bd.items()}}
 
     beam = config3 = None
     if not args.no_beam:

@@ -23,9 +23,11 @@ CLASS_OF = {
     "input_proj": (("gemm16_persist_kernel", "gemm16_bias_kernel"), 4),
     "rec_step": (("rec_layer_kernel",), 4),
     "keys": (("gemm_nt_kernel<KeysEpi",), 1),
-    "dec_lstm": (("dgemm_kernel<2, 4, 4, DecLstmA", "dgemm_kernel<4, 4, 4, DecLstmA", "dgemm_kernel<8, 4, 3, DecLstmA"), 40),
+    "dec_lstm": (("dgemm_kernel<2, 4, 4, DecLstmA", "dgemm_kernel<4, 4, 4, DecLstmA", "dgemm_kernel<8, 8, 4, DecLstmA",
+                  "dgemm_kernel<8, 8, 2, DecLstmA"), 40),
     "proj": (("dgemm_kernel<2, 5, 4, ProjA", "dgemm_kernel<4, 5, 4, ProjA", "dgemm_kernel<8, 5, 3, ProjA",
-              "dgemm_kernel<4, 10, 2, ProjA"), 40),
+              "dgemm_kernel<4, 10, 2, ProjA", "dgemm_kernel<8, 10, 3, ProjA"), 40),
+    "select": (("beam_select_kernel",), 40),
     "attention": (("attention_kernel",), 40),
     "features": (("features_stats_kernel", "features_rows_kernel"), 1),
 }

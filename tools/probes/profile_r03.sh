@@ -1,6 +1,7 @@
 # Round-3 evidence on one box (profiles/r03): the default bench line; rocprofv3 kernel trace +
 # stats of a greedy-only bench run (its dominant kernel's average must agree with the line's
-# HIP-event figure: 20 timed steps dominate the 3 untimed ones); PMC passes of two greedy steps.
+# HIP-event figure: 20 timed steps dominate the 3 untimed ones) and of three beam 8 B = 256
+# steps; PMC passes of two greedy steps and of two beam 8 B = 256 steps.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/r03
@@ -15,11 +16,20 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pro
 python tools/prof_by_grid.py $O/prof/run_kernel_trace.csv 30 > $O/prof_by_grid.txt 2>&1
 head -12 $O/prof_by_grid.txt
 R=$GRAFT_REPO_ROOT
-P=$O/pmc
-mkdir -p $P
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d $P/p1 -o p1 -- python3 $R/tools/probes/one_step.py > $P/p1.log 2>&1 || { tail -3 $P/p1.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/p2 -o p2 -- python3 $R/tools/probes/one_step.py > $P/p2.log 2>&1 || { tail -3 $P/p2.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/p3 -o p3 -- python3 $R/tools/probes/one_step.py > $P/p3.log 2>&1 || { tail -3 $P/p3.log; exit 1; }
-python tools/pmc_summary.py $P --json $O/pmc_traffic.json > $O/pmc_summary.txt 2>&1
+STEPS=3 BEAM=8 B=256 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_beam -o run -- \
+  python3 $R/tools/probes/one_step.py > $O/prof_beam.log 2>&1 || { tail -5 $O/prof_beam.log; exit 1; }
+python tools/prof_by_grid.py $O/prof_beam/run_kernel_trace.csv 30 > $O/prof_beam_by_grid.txt 2>&1
+head -12 $O/prof_beam_by_grid.txt
+for mode in greedy beam; do
+  P=$O/pmc_$mode
+  mkdir -p $P
+  if [ $mode = beam ]; then export BEAM=8 B=256; else unset BEAM; export B=256; fi
+  timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d $P/p1 -o p1 -- python3 $R/tools/probes/one_step.py > $P/p1.log 2>&1 || { tail -3 $P/p1.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/p2 -o p2 -- python3 $R/tools/probes/one_step.py > $P/p2.log 2>&1 || { tail -3 $P/p2.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/p3 -o p3 -- python3 $R/tools/probes/one_step.py > $P/p3.log 2>&1 || { tail -3 $P/p3.log; exit 1; }
+done
+unset BEAM
+python tools/pmc_summary.py $O/pmc_greedy --json $O/pmc_traffic.json > $O/pmc_summary.txt 2>&1
+python tools/pmc_summary.py $O/pmc_beam --json $O/pmc_traffic_beam.json > $O/pmc_summary_beam.txt 2>&1
 head -14 $O/pmc_summary.txt
-cat $O/pmc_traffic.json | head -50
+head -14 $O/pmc_summary_beam.txt
