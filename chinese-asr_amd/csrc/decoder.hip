@@ -1580,11 +1580,10 @@ static void launch_dec_lstm(int R, const float* Wf, const ASrc& asrc, const Epi&
   const int NB = HD / 16, ntiles = 4 * NB, nkt = KDEC / DG_BK;
   if (R <= 256) launch_dg<2, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 512) launch_dg<4, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  // R > 512: 128 rows x 128 columns (two 16-unit groups): at R = 2048 one round of 256 blocks,
-  // 1.3 MB per block, instead of two rounds of 128 x 64 blocks (ring 3) at 0.98 MB each; s16: a
-  // ring of four 32-deep stages (three in flight), f32: two 64-deep stages
-  else if (!s16) launch_dg<8, 8, 2, 1, 1, true>(NB / 2, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  else launch_dg<8, 8, 4, 1, 1, true, 32>(NB / 2, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  // R > 512: 128 rows x 128 columns (two 16-unit groups), two 64-deep stages: at R = 2048 one
+  // round of 256 blocks, 1.3 MB per block, instead of two rounds of 128 x 64 blocks (ring 3) at
+  // 0.98 MB each
+  else launch_dg<8, 8, 2, 1, 1, true>(NB / 2, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
 template <class ASrc, class Epi>
