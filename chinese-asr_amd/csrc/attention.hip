@@ -128,9 +128,18 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       float4 pv[AT_NQ];
 #pragma unroll
       for (int p = 0; p < AT_NQ; ++p) pv[p] = p < nq ? qp[(size_t)p * R * (A / 4)] : make_float4(0.f, 0.f, 0.f, 0.f);
+      // 16-unit slots are summed in pairs first: a 32-unit slot (dec_q_slots) holds exactly that
+      // pair sum, so q has the same bits whichever LSTMCell shape wrote the partials
+      if (nq == AT_NQ) {
 #pragma unroll
-      for (int p = 0; p < AT_NQ; ++p)
-        if (p < nq) q.x += pv[p].x, q.y += pv[p].y, q.z += pv[p].z, q.w += pv[p].w;
+        for (int p = 0; p < AT_NQ; p += 2)
+          q.x += pv[p].x + pv[p + 1].x, q.y += pv[p].y + pv[p + 1].y, q.z += pv[p].z + pv[p + 1].z,
+              q.w += pv[p].w + pv[p + 1].w;
+      } else {
+#pragma unroll
+        for (int p = 0; p < AT_NQ / 2; ++p)
+          if (p < nq) q.x += pv[p].x, q.y += pv[p].y, q.z += pv[p].z, q.w += pv[p].w;
+      }
     }
     qs[(4 * a4 + 0) * KPB + j] = q.x;
     qs[(4 * a4 + 1) * KPB + j] = q.y;

@@ -303,9 +303,12 @@ struct DecodeArgs {
 };
 
 // attention.hip: one decode step's additive attention for all R rows (writes ctx into st)
+// decode rows at which the LSTMCell (128 x 128) and projection (256 x 160) blocks of decoder.hip
+// fill the CUs in one round; below it the narrower blocks do
+inline bool dec_wide(int R) { return R >= 2048; }
 // attention query partials per decoder row: one per LSTMCell column block (decoder.hip
-// launch_dec_lstm), 16 units each at R <= 512, 32 units at R > 512
-inline int dec_q_slots(int R) { return R > 512 ? HD / 32 : HD / 16; }
+// launch_dec_lstm), 16 units each, 32 units at dec_wide(R)
+inline int dec_q_slots(int R) { return dec_wide(R) ? HD / 32 : HD / 16; }
 hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
                                  int32_t* newdone, int l, int total, hipStream_t s);
 size_t attention_smem_bytes(int B, int k, int Tp, int opt);

@@ -593,9 +593,11 @@ struct DecLstmEpi {
   __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p, float*) const {
     static_assert(NTN % 4 == 0 && NTN / 4 <= UGMAX, "the LSTM cell needs the 4 gate tiles of each 16-unit group");
     constexpr int UG = NTN / 4;
-    // per row-slab wave (<= 8 per block): the h tile [row][unit] of its UG unit groups; the query
-    // partial of the block's 16 UG units is one MFMA chain over them (qpart slot nb, dec_q_slots)
-    __shared__ float ht[8][16][16 * UGMAX + 1];
+    // per row-slab wave (<= 8 per block): the h tile [row][unit] of its UG unit groups.  The query
+    // partial of each 16-unit group is its own MFMA chain; a two-group block stores their sum in
+    // slot nb (dec_q_slots), which is the pair sum the attention forms from two 16-unit slots, so
+    // q has the same bits at every R
+    __shared__ float ht[8][16][16 * UG + 1];
     const int lane = threadIdx.x & 63, ws = (row0 >> 4) & 7, g = lane >> 4;
     const int rbase = row0 - 4 * g;  // first row of this wave's slab
 #pragma unroll
@@ -626,9 +628,13 @@ struct DecLstmEpi {
     for (int at = 0; at < A / 16; ++at) {
       f32x4 q = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ug = 0; ug < UG; ++ug)
+      for (int ug = 0; ug < UG; ++ug) {
+        f32x4 qg = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) q = mfma16x16x4(ht[ws][lane & 15][16 * ug + 4 * kk + g], p.wh[ug][at][kk], q);
+        for (int kk = 0; kk < 4; ++kk) qg = mfma16x16x4(ht[ws][lane & 15][16 * ug + 4 * kk + g], p.wh[ug][at][kk], qg);
+        if (ug == 0) q = qg;
+        else q += qg;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = rbase + 4 * g + e;
@@ -1580,9 +1586,10 @@ static void launch_dec_lstm(int R, const float* Wf, const ASrc& asrc, const Epi&
   const int NB = HD / 16, ntiles = 4 * NB, nkt = KDEC / DG_BK;
   if (R <= 256) launch_dg<2, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 512) launch_dg<4, 4, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  // R > 512: 128 rows x 128 columns (two 16-unit groups), two 64-deep stages: at R = 2048 one
+  else if (!dec_wide(R)) launch_dg<8, 4, 3, 1, 1, true>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  // R >= 2048: 128 rows x 128 columns (two 16-unit groups), two 64-deep stages: at R = 2048 one
   // round of 256 blocks, 1.3 MB per block, instead of two rounds of 128 x 64 blocks (ring 3) at
-  // 0.98 MB each
+  // 0.98 MB each (at R = 1024 the 128 x 64 blocks are one round: 256 blocks)
   else launch_dg<8, 8, 2, 1, 1, true>(NB / 2, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
@@ -1595,10 +1602,11 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
   else if (R <= 256) launch_dg<4, 5, 4>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (R <= 512) launch_dg<8, 5, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   else if (!s16 || !small_w) launch_dg<4, 10, 2, 2, 2, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
-  // s16 at R > 512 with |W_p| < 16: 256 x 160 blocks of 32-deep stages, ring 3, one accumulator
+  else if (!dec_wide(R)) launch_dg<4, 10, 2, 2, 2, true, 64, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  // s16 at R >= 2048 with |W_p| < 16: 256 x 160 blocks of 32-deep stages, ring 3, one accumulator
   // (one round of 256 blocks at R = 2048, 1.7 MB per block, against two rounds of 128 x 160 blocks
-  // at 1.2 MB each)
-  else launch_dg<8, 10, 3, 2, 1, true, 32, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+  // at 1.2 MB each; at R = 1024 the 128 x 160 blocks are one round: 256 blocks)
+  else launch_dg<4, 10, 3, 4, 2, true, 32, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
 // ------------------------------------------------------------------ host drivers
@@ -1606,9 +1614,10 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
 // blocks; beam search uses them at temperature 1 only (they are of x, not x / T)
 static int proj_col_blocks(const DecodeArgs& a) {
   const int nt = a.L.VP / 16, R = a.B * a.k;
-  // the column block of a wave (ProjEpi's partial index): 5 tiles, 10 for the one-accumulator
-  // 256 x 160 beam block (launch_proj: s16, R > 512, |W_p| < 16)
-  return a.s16 && a.proj_small && R > 512 ? (nt + 9) / 10 : (nt + 4) / 5;
+  // the column block of a wave (ProjEpi's partial index): 5 tiles in every launch_proj shape (the
+  // beam blocks' two wave columns), so the select's partial sums do not depend on R
+  (void)R;
+  return (nt + 4) / 5;
 }
 static bool row_partials(const DecodeArgs& a) {
   return proj_col_blocks(a) <= GP_NB && (a.greedy_run || a.temperature == 1.0f);
