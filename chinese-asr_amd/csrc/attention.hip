@@ -36,10 +36,16 @@ __host__ __device__ constexpr int attn_scratch_floats(int Tq) {
   return AT_MAXG * KPB * Tq > 4 * KPB * C ? AT_MAXG * KPB * Tq : 4 * KPB * C;
 }
 
-// LDS: qs, eqs [AT_APAD][KPB] | vs, v2s [A] | (AT_MAXG unused) | scratch | es [Tq][KPB] | value rows
-template <int KPB>
+// the folded step's cell phase (CELL): h [HD] | query slices [AT_QS][A]
+constexpr int AT_QS = AT_THREADS / (A / 4);  // 16 unit slices of HD / AT_QS = 32 units
+constexpr int AT_CELL_FLOATS = HD + AT_QS * A;
+
+// LDS: qs, eqs [AT_APAD][KPB] | vs, v2s [A] | (AT_MAXG unused) | scratch | es [Tq][KPB] | (CELL: h,
+// query slices) | value rows
+template <int KPB, bool CELL = false>
 __host__ __device__ constexpr size_t attn_smem_floats(int Tp) {
-  return (size_t)2 * KPB * AT_APAD + 2 * A + AT_MAXG + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp);
+  return (size_t)2 * KPB * AT_APAD + 2 * A + AT_MAXG + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp) +
+         (CELL ? AT_CELL_FLOATS : 0);
 }
 
 // Split exponential form of the score tanh.  tanh(k + q) = 1 - 2 / (1 + e^{2k} e^{2q}): with
@@ -89,19 +95,24 @@ CASR_DEV f32x2 tanh_fast2(f32x2 x) {
 // diagnostics (CASR_DG_TRACE, tools/probes/dg_trace.py): per-block phase stamps of the last launch
 __device__ uint32_t* g_at_trace = nullptr;
 
-template <int KPB>
+// CELL (the folded greedy step, casr_internal.h KA; KPB = 1, row r = b): before the attention the
+// block runs the select of step l - 1 for its row, the LSTM cell on gates_prev[r] + emb_gates[tok]
+// and q = h . W_hidden itself (no query partials); st receives h, c (and ctx as always).
+template <int KPB, bool CELL = false>
 __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float* __restrict__ st, const float* __restrict__ qpart, const float* __restrict__ keysT,
     const float* __restrict__ ekT, const float* __restrict__ enc, const int32_t* __restrict__ lens,
     const float* __restrict__ vv, int R, int k, int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone,
-    int l, int total, int npf, int direct, int nq) {
+    int l, int total, int npf, int direct, int nq, int V, AttnCell cell) {
+  static_assert(!CELL || KPB == 1, "the folded step is greedy: one row per block");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   uint32_t* atr = g_at_trace ? g_at_trace + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int i) {
     if (atr && threadIdx.x == 0) atr[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  if (done_before(newdone, l) >= total) return;
+  // (CELL: the early exit is decided after the block's own select, below)
+  if (!CELL && done_before(newdone, l) >= total) return;
   const int Tq = attn_tq(Tp);
   float* qs = sm;                   // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
   float* eqs = qs + KPB * AT_APAD;  // [AT_APAD][KPB]: exp(2q) (split form), zero past A
@@ -109,18 +120,116 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   float* v2s = vs + A;              // [A]: -2 v
   float* xs = v2s + A + AT_MAXG;    // scratch
   float* es = xs + attn_scratch_floats<KPB>(Tq);  // [Tq][KPB]: one 4 x KPB-byte read per t
-  float* vl = es + KPB * Tq;                       // [npf][C]: value rows 0..npf-1 (LDS-DMA)
+  float* hs = es + KPB * Tq;                       // CELL: [HD] h, then [AT_QS][A] query slices
+  float* vl = hs + (CELL ? AT_CELL_FLOATS : 0);    // [npf][C]: value rows 0..npf-1 (LDS-DMA)
   const int b = blockIdx.x, j0 = blockIdx.y * KPB;
   const int nk = min(KPB, k - j0);
   const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
   const int len = min(lens[b], Tp);
   const size_t row0 = (size_t)b * k + j0;
 
+  if constexpr (CELL) {
+    // 0. the folded step's LSTM cell (decoder.py:104-114) and query (attention.py:92) for row r.
+    // W_hidden slice (rows 32 us .. +31, columns 4 a4 .. +3), the previous step's gate
+    // pre-activations of unit u = tid and its c are loaded first: none depends on the select
+    __shared__ int tk_s, skip_s;
+    const int r = (int)row0;
+    const int a4 = tid & (A / 4 - 1), us = tid / (A / 4);
+    constexpr int UPS = HD / AT_QS;  // units per query slice
+    float4 wh[UPS];
+#pragma unroll
+    for (int i = 0; i < UPS; ++i)
+      wh[i] = *reinterpret_cast<const float4*>(cell.w_hidden + (size_t)(UPS * us + i) * A + 4 * a4);
+    const int u = tid;
+    auto gcol = [](int g, int u) { return (u >> 4) * 64 + g * 16 + (u & 15); };  // packed_gate_row
+    float gprev[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) gprev[g] = cell.gates[(size_t)r * (4 * HD) + gcol(g, u)];
+    const float cold = cell.st_old[(size_t)r * ST + C + HD + u];
+    if (wv == 0) {  // the select of step l - 1 (greedy_select_part_kernel's arithmetic) and its bookkeeping
+      int t = 0;
+      if (cell.sel) {
+        const GreedySel& gs = cell.gs;
+        float m = -INFINITY, se = 0.f;
+        int mi = 0x7fffffff;
+        if (ln < gs.nbp) {
+          m = gs.gp.mx[(size_t)r * GP_NB + ln];
+          se = gs.gp.se[(size_t)r * GP_NB + ln];
+          mi = gs.gp.ix[(size_t)r * GP_NB + ln];
+        }
+        uint8_t fin0 = 0;
+        float acc0 = 0.f;
+        int len0 = 0;
+        if (ln == 0) {
+          fin0 = gs.fin[r];
+          acc0 = gs.accum[r];
+          len0 = gs.out_len[r];
+        }
+        if (done_before(gs.newdone, gs.lsel) < total) {  // else nothing downstream runs any more
+          float gm = m;
+          int gi = mi;
+          wave_best(gm, gi);
+          t = gi;
+          const bool bad_t = (unsigned)t >= (unsigned)V;  // no finite maximum (NaN row)
+          if (bad_t) t = 0;
+          const float sx = wave_sum((se > 0.f) ? se * expf(m - gm) : 0.f);
+          if (ln == 0) {
+            if (bad_t) atomicOr(cell.err, CASR_DEV_NAN_LOGITS);
+            greedy_book(gs, r, t, gm - (logf(sx) + gm), fin0, acc0, len0);
+          }
+        }
+      } else {
+        t = cell.tok[r];
+        if ((unsigned)t >= (unsigned)V) {
+          if (ln == 0) atomicOr(cell.err, CASR_DEV_BAD_TOKEN);
+          t = 0;
+        }
+      }
+      // after this wave's own bookkeeping: rows finished before step l (a block that sees them all
+      // skips work nothing downstream reads; one that does not computes it)
+      const int dn = done_before(newdone, l);
+      if (ln == 0) {
+        tk_s = t;
+        skip_s = dn >= total;
+      }
+    }
+    __syncthreads();
+    if (skip_s) return;
+    const int t = tk_s;
+    float eg[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) eg[g] = cell.emb_gates[(size_t)t * (4 * HD) + gcol(g, u)];
+    float h2, c2;
+    lstm_cell_hw(gprev[0] + eg[0], gprev[1] + eg[1], gprev[2] + eg[2], gprev[3] + eg[3], cold, h2, c2);
+    st[(size_t)r * ST + C + u] = h2;
+    st[(size_t)r * ST + C + HD + u] = c2;
+    reinterpret_cast<uint32_t*>(st)[(size_t)r * ST + ST16 + C + u] = split16_word(h2);
+    hs[u] = h2;
+    __syncthreads();
+    float4 qa = make_float4(0.f, 0.f, 0.f, 0.f);  // units in order within the slice
+#pragma unroll
+    for (int i = 0; i < UPS; ++i) {
+      const float hv = hs[UPS * us + i];
+      qa.x = fmaf(hv, wh[i].x, qa.x);
+      qa.y = fmaf(hv, wh[i].y, qa.y);
+      qa.z = fmaf(hv, wh[i].z, qa.z);
+      qa.w = fmaf(hv, wh[i].w, qa.w);
+    }
+    *reinterpret_cast<float4*>(hs + HD + us * A + 4 * a4) = qa;
+    __syncthreads();
+    for (int a = tid; a < A; a += AT_THREADS) {  // slices added in slice order
+      float q = hs[HD + a];
+#pragma unroll
+      for (int i = 1; i < AT_QS; ++i) q += hs[HD + i * A + a];
+      qs[a] = q;
+      eqs[a] = split_exp2x(q);
+    }
+  }
   // 1. q = sum of the HD/16 partials in partial order (p = 0, 1, ...), v -> LDS.  The block's
   // KPB rows are consecutive, so partial p of all of them is one contiguous KPB x A span: a thread
   // takes one float4 (row j, columns 4 a4..4 a4 + 3) and has its AT_NQ 16-B loads in flight at
   // once (one round trip; the zero pad rows a >= A take no loads)
-  for (int f = tid; f < KPB * (A / 4); f += AT_THREADS) {
+  for (int f = tid; !CELL && f < KPB * (A / 4); f += AT_THREADS) {
     const int j = f / (A / 4), a4 = f - j * (A / 4);
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     if (j < nk) {
@@ -477,33 +586,39 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 // budget (two blocks per CU) unchanged; the knob was removed in round 3.
 static size_t attn_lds_budget() { return (size_t)156 * 1024; }
 
-template <int KPB>
+template <int KPB, bool CELL = false>
 static int attn_npf(int Tp) {
-  const size_t fixed = attn_smem_floats<KPB>(Tp) * sizeof(float);
+  const size_t fixed = attn_smem_floats<KPB, CELL>(Tp) * sizeof(float);
   const size_t budget = attn_lds_budget();
   const size_t room = fixed < budget ? budget - fixed : 0;
   const int rows = (int)(room / (C * sizeof(float))) & ~3;
   return rows < Tp ? rows : (Tp + 3) & ~3;
 }
 
-template <int KPB>
+template <int KPB, bool CELL = false>
 static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart, float* align, int32_t* newdone,
-                             int l, int total, hipStream_t s) {
-  const int npf = attn_npf<KPB>(a.Tp);
-  const size_t shm = (attn_smem_floats<KPB>(a.Tp) + (size_t)npf * C) * sizeof(float);
+                             int l, int total, hipStream_t s, const AttnCell& cell = AttnCell{}) {
+  const int npf = attn_npf<KPB, CELL>(a.Tp);
+  const size_t shm = (attn_smem_floats<KPB, CELL>(a.Tp) + (size_t)npf * C) * sizeof(float);
   static size_t raised = 0;  // allow > 64 KiB of dynamic LDS (160 KiB per CU on gfx950)
   if (shm > raised) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(attention_kernel<KPB>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(attention_kernel<KPB, CELL>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     if (e != hipSuccess) return e;
     raised = shm;
   }
   dim3 grid(a.B, (a.k + KPB - 1) / KPB);
   const float* ekT = a.keysT + (size_t)a.B * A * attn_tq(a.Tp);  // KeysEpi: [keys | exp(2 keys)]
-  hipLaunchKernelGGL(attention_kernel<KPB>, grid, dim3(AT_THREADS), shm, s, st, qpart, a.keysT, ekT, a.enc, a.lens,
-                     a.W + a.L.v, a.B * a.k, a.k, a.Tp, align, newdone, l, total, npf, a.attn_direct,
-                     dec_q_slots(a.B * a.k));
+  hipLaunchKernelGGL((attention_kernel<KPB, CELL>), grid, dim3(AT_THREADS), shm, s, st, qpart, a.keysT, ekT, a.enc,
+                     a.lens, a.W + a.L.v, a.B * a.k, a.k, a.Tp, align, newdone, l, total, npf, a.attn_direct,
+                     dec_q_slots(a.B * a.k), a.V, cell);
   return hipGetLastError();
+}
+
+hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const AttnCell& cell, float* align,
+                                      int32_t* newdone, int l, int total, hipStream_t s) {
+  if (a.k != 1) return hipErrorInvalidValue;  // greedy only
+  return launch_kpb<1, true>(a, st, nullptr, align, newdone, l, total, s, cell);
 }
 
 // beam rows per block at k > 2 (CASR_OPT_ATTN_KPB, 0 = auto).  4 rows per block at B < 256: 8 rows

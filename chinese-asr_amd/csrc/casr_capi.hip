@@ -174,6 +174,10 @@ struct casr_handle {
   bool s16_valid = false;           // the bound blob's s16 images are usable (Layout::info)
   bool proj_small = false;          // every |W_p| < 16 (Layout::info + 4)
   DevBuf x16;                       // s16 row image of the current layer input [B*Tp][Kp]
+  // folded greedy decode (CASR_OPT_DEC_FOLD): fused projection | LSTM-gate fragment image and the
+  // per-token gate table, built at bind from an s16-valid blob; the gates buffer [R][4 HD]
+  DevBuf wfold, egates, fgates;
+  bool fold_ready = false;
   bool s16() const { return precision == CASR_PREC_S16X3 && s16_valid; }
   int B = 0, Tp = 0;
   bool encoded = false;
@@ -445,6 +449,17 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
   h->proj_small = info[4] == 1.f;
   h->W = packed_device;
   h->graphs.clear();  // captured graphs bake in the precision and weight pointers
+  // the folded greedy step's tables (decoder.hip build_fold): derived from this blob, so rebuilt
+  // at every bind; a blob without valid s16 images keeps the three-launch step
+  h->fold_ready = false;
+  if (h->s16_valid) {
+    const int V = h->cfg.vocab;
+    HIP_OK(h, h->wfold.ensure((size_t)(fold_vtiles(V) + FOLD_GT) * (KPROJ / 64) * FRAG * sizeof(float)));
+    HIP_OK(h, h->egates.ensure((size_t)V * 4 * HD * sizeof(float)));
+    HIP_OK(h, build_fold(h->W, h->L, V, h->wfold.as<float>(), h->egates.as<float>(), nullptr));
+    HIP_OK(h, hipStreamSynchronize(nullptr));
+    h->fold_ready = true;
+  }
   return CASR_OK;
 }
 
@@ -472,7 +487,8 @@ void casr_destroy(casr_handle* h) {
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->gflags, &h->fe_const,
-                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout})
+                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout, &h->wfold,
+                    &h->egates, &h->fgates})
     b->release();
   delete h;
 }
@@ -506,8 +522,8 @@ int casr_recurrence_mode(const casr_handle* h, int B) {
 int casr_set_option(casr_handle* h, int option, int value) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
-  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0};
-  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8, 1};
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8, 1, 1};
   if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
     return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
   if (value < lo[option] || value > hi[option])
@@ -878,6 +894,12 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   a.attn_kpb = h->tune[CASR_OPT_ATTN_KPB];
   a.attn_direct = h->tune[CASR_OPT_ATTN_DIRECT];
   a.proj_small = h->proj_small;
+  // the folded greedy step (greedy only: casr_greedy passes k = 1; run_beam ignores it)
+  a.fold = k == 1 && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
+  if (a.fold) {
+    HIP_OK(h, h->fgates.ensure((size_t)R * 4 * HD * sizeof(float)));
+    a.fb = FoldBufs{h->wfold.as<float>(), h->egates.as<float>(), h->fgates.as<float>()};
+  }
   return CASR_OK;
 }
 
@@ -905,7 +927,7 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   float* ial = align ? iacc + B : nullptr;
   uint8_t* ifin = reinterpret_cast<uint8_t*>(iacc + B + nal);
   a.prof = nullptr;
-  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
+  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)a.fold, (uint64_t)h->fgates.p, (uint64_t)h->wfold.p, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
                                      (uint64_t)(align != nullptr), (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->enc_out, (uint64_t)h->keysT.p,
                                      (uint64_t)h->hfin.p, (uint64_t)h->cst.p, (uint64_t)h->lens.p};

@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0, 0};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0, 0, 1};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -262,6 +262,62 @@ struct GreedyPart {
 };
 constexpr int GP_NT = 320;  // 16-column tiles per row (V <= 5120)
 
+// Greedy select of step lsel fused into a later kernel of step lsel + 1 (the LSTMCell GEMM's
+// prologue, decoder.hip DecLstmA; or the folded step's attention kernel, attention.hip): the
+// projection's per-block row partials of step lsel are reduced by the consumer itself and the
+// bookkeeping of greedy_select_part_kernel (model.py:540-590) is done by one writer per row.
+struct GreedySel {
+  GreedyPart gp;
+  int nbp, lsel, L, eos;
+  uint8_t* fin;
+  int32_t* out_len;
+  float* accum;
+  int32_t* tokens;
+  int32_t* newdone;
+};
+
+#ifdef __HIPCC__
+// the writer's bookkeeping of row r once its token t and log-probability lp are known (lane 0
+// only): tokens, finished, lengths, score and the newly-finished counter, as model.py:554-578
+__device__ __forceinline__ void greedy_book(const GreedySel& gs, int r, int t, float lp, uint8_t fin0, float acc0,
+                                            int len0) {
+  gs.tokens[(size_t)r * gs.L + gs.lsel] = t;
+  const bool was = fin0 != 0;
+  const bool cur = t == gs.eos;
+  float acc = acc0;
+  if (!was && cur) acc = acc + lp;  // model.py:567
+  const bool now = was || cur;
+  if (!now) {
+    gs.out_len[r] = len0 + 1;  // model.py:573
+    acc = acc + lp;            // model.py:576
+  }
+  gs.accum[r] = acc;
+  if (now && !was) {
+    gs.fin[r] = 1;
+    atomicAdd(&gs.newdone[gs.lsel], 1);
+  }
+}
+#endif
+
+// Folded greedy decode (CASR_OPT_DEC_FOLD): per step l >= 1 two launches instead of three.
+//   KA (attention.hip, attention_kernel<1, true>): select of step l-1 from the projection
+//      partials, gates = gates_prev[r] + emb_gates[tok] (the per-token table: emb . W_emb^T +
+//      b_ih + b_hh), the LSTM cell, q = h . W_hidden by f32 fma chains, then the attention.
+//   KB (decoder.hip, dgemm_kernel<.., FoldEpi>): [ctx | h] . [W_p ; W_ch]^T on one fused
+//      fragment image: the vocabulary tiles (greedy partials) and the LSTM gate tiles of the next
+//      step (K = 1024: the ctx | h part of the LSTM contraction, decoder.py:104-114), one GEMM
+//      over the same A rows.
+constexpr int FOLD_GT = 4 * HD / 16;  // LSTM gate tiles (16 gate rows each) in the fused image
+constexpr int FOLD_NT = 7;            // 16-column tiles per fused GEMM block (112 columns)
+inline int fold_vtiles(int V) { return (V + 15) / 16; }
+struct FoldBufs {
+  const float* wfold;      // s16 fragment image: [fold_vtiles(V) + FOLD_GT tiles][KPROJ / 64] FRAG blocks
+  const float* emb_gates;  // [V][4 HD] packed gate-row order (packed_gate_row), biases included
+  float* gates;            // [R][4 HD] the next step's [ctx | h] . W_ch^T, packed gate-row order
+};
+// build the fused image and the per-token gate table from a bound s16-valid blob (bind time)
+hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, hipStream_t s);
+
 struct DecodeBufs {
   float* st[2];          // [R][ST]
   float* logits;         // [R][V]
@@ -300,6 +356,8 @@ struct DecodeArgs {
   int attn_kpb;          // CASR_OPT_ATTN_KPB (0 auto)
   int attn_direct;       // CASR_OPT_ATTN_DIRECT
   int proj_small;        // every |W_p| < 16 (blob info word 4): the one-accumulator s16x3 projection
+  int fold;              // CASR_OPT_DEC_FOLD in effect (greedy, s16x3, tables built)
+  FoldBufs fb;           // fold tables and the gates buffer (fold only)
 };
 
 // attention.hip: one decode step's additive attention for all R rows (writes ctx into st)
@@ -311,6 +369,20 @@ inline bool dec_wide(int R) { return R >= 2048; }
 inline int dec_q_slots(int R) { return dec_wide(R) ? HD / 32 : HD / 16; }
 hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
                                  int32_t* newdone, int l, int total, hipStream_t s);
+// the folded step's attention (KA above): st_old supplies c, st receives h, c and ctx; sel: the
+// fused select of step gs.lsel (else tokens from tok)
+struct AttnCell {
+  const float* st_old;
+  const float* gates;
+  const float* emb_gates;
+  const float* w_hidden;  // [HD][A]
+  const int32_t* tok;     // sel == 0
+  int32_t* err;
+  int sel;
+  GreedySel gs;
+};
+hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const AttnCell& cell, float* align,
+                                      int32_t* newdone, int l, int total, hipStream_t s);
 size_t attention_smem_bytes(int B, int k, int Tp, int opt);
 int attention_kpb(int B, int k, int opt);  // beam rows per attention block
 void attn_trace_bind(uint32_t* buf);  // CASR_DG_TRACE diagnostics (attention.hip)

@@ -425,16 +425,7 @@ static void launch_dg(int NB, int R, int ntiles, int nkt, const float* Wf, const
 // tokens (32 rows x 64 partials); the block with nb == 0 also does the bookkeeping of
 // greedy_select_part_kernel (tokens, finished, lengths, score, newdone), with the same
 // arithmetic, so both forms give the same bits.
-struct GreedySel {
-  GreedyPart gp;
-  int nbp, lsel, L, eos;
-  uint8_t* fin;
-  int32_t* out_len;
-  float* accum;
-  int32_t* tokens;
-  int32_t* newdone;
-};
-
+// (GreedySel, greedy_book: casr_internal.h)
 __device__ __forceinline__ int* sel_tok_lds() {
   __shared__ int t[128];
   return t;
@@ -499,21 +490,7 @@ struct DecLstmA {
       if (lane != 0) continue;
       if (bad_t) atomicOr(err, CASR_DEV_NAN_LOGITS);
       const float lp = gm - (logf(sx) + gm);
-      gs.tokens[(size_t)r * gs.L + gs.lsel] = t;
-      const bool was = fin0[i] != 0;
-      const bool cur = t == gs.eos;
-      float acc = acc0[i];
-      if (!was && cur) acc = acc + lp;  // model.py:567
-      const bool now = was || cur;
-      if (!now) {
-        gs.out_len[r] = len0[i] + 1;  // model.py:573
-        acc = acc + lp;               // model.py:576
-      }
-      gs.accum[r] = acc;
-      if (now && !was) {
-        gs.fin[r] = 1;
-        atomicAdd(&gs.newdone[gs.lsel], 1);
-      }
+      greedy_book(gs, r, t, lp, fin0[i], acc0[i], len0[i]);
     }
     __syncthreads();
   }
@@ -771,6 +748,140 @@ struct ProjEpi {
     }
   }
 };
+
+// Epilogue of the folded step's GEMM (casr_internal.h KB): columns are 16-column tiles of the
+// fused image, vocabulary tiles T < VT first (greedy partials exactly as ProjEpi's, over the
+// tile's columns n < V), then the LSTM gate tiles gt = T - VT of the next step, stored raw into
+// gates[row][gt * 16 + u] (packed gate-row order; the biases are in the per-token table).  A block
+// whose tiles are all gate tiles writes no partial; nbp = ceil(VT / NT) blocks do.
+struct FoldEpi {
+  static constexpr int kTraceClass = 1;
+  static constexpr bool kScratch = false;
+  const float* bias;  // proj_b [VP]
+  const int32_t* newdone;
+  int R, V, VT, l, total;
+  int32_t* err;
+  GreedyPart gp;
+  float* gates;  // [R][4 HD]
+  struct Pre {
+    float bn[16];
+  };
+  __device__ __forceinline__ int32_t* err_flags() const { return err; }
+  __device__ __forceinline__ bool skip() const { return done_before(newdone, l) >= total; }
+  template <int NTN>
+  __device__ __forceinline__ void prefetch(Pre& p, int, int nb, int u, int&) const {
+    static_assert(NTN <= 16, "bias prefetch slots");
+#pragma unroll
+    for (int tn = 0; tn < NTN; ++tn) {
+      const int n = (nb * NTN + tn) * 16 + u;
+      p.bn[tn] = n < V ? bias[n] : 0.f;
+    }
+  }
+  template <int NTN>
+  __device__ __forceinline__ void late(Pre&, int, int, int) const {}
+  template <int NTN>
+  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p, float*) const {
+#pragma unroll
+    for (int tn = 0; tn < NTN; ++tn) {
+      const int gt = nb * NTN + tn - VT;
+      if (gt < 0 || gt >= FOLD_GT) continue;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = row0 + e;
+        if (row < R) gates[(size_t)row * (4 * HD) + gt * 16 + u] = acc[tn][e];
+      }
+    }
+    if (nb * NTN >= VT) return;  // no vocabulary tile in this block
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x[NTN];
+      float m = -INFINITY;
+      int mi = 0x7fffffff;
+#pragma unroll
+      for (int tn = 0; tn < NTN; ++tn) {
+        const int n = (nb * NTN + tn) * 16 + u;
+        x[tn] = acc[tn][e] + p.bn[tn];
+        if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
+          m = x[tn];
+          mi = n;
+        }
+      }
+      {
+        const float rm = row16_max(m);
+        mi = row16_min(m == rm ? mi : 0x7fffffff);
+        m = rm;
+      }
+      float sx = 0.f;
+#pragma unroll
+      for (int tn = 0; tn < NTN; ++tn) {
+        const int n = (nb * NTN + tn) * 16 + u;
+        if (n < V) sx += expf(x[tn] - m);
+      }
+      sx = row16_sum(sx);
+      const int row = row0 + e;
+      if (u == 0 && row < R) {
+        gp.mx[(size_t)row * GP_NB + nb] = m;
+        gp.se[(size_t)row * GP_NB + nb] = sx;
+        gp.ix[(size_t)row * GP_NB + nb] = mi;
+      }
+    }
+  }
+};
+
+// ------------------------------------------------------------------ fold tables (bind time)
+// the fused fragment image: vocabulary tiles 0..VT-1 of proj_w16, then the 128 LSTM gate tiles of
+// dec_w16 restricted to its k blocks 4..19 (the [ctx | h] part of [emb | ctx | h]: E = 256 = 4 x 64)
+__global__ void fold_image_kernel(const float* __restrict__ proj16, const float* __restrict__ dec16, int VT,
+                                  float* __restrict__ out) {
+  const int T = blockIdx.x / (KPROJ / 64), kc = blockIdx.x % (KPROJ / 64);
+  const float* src = T < VT ? proj16 + ((size_t)T * (KPROJ / 64) + kc) * FRAG
+                            : dec16 + ((size_t)(T - VT) * (KDEC / 64) + E / 64 + kc) * FRAG;
+  float* dst = out + (size_t)blockIdx.x * FRAG;
+  for (int i = threadIdx.x; i < FRAG / 4; i += blockDim.x)
+    reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+}
+
+// the per-token gate table: emb_gates[v][n] = sum_k emb[v][k] W_dec[n][k] (k < E, f32 fma chain
+// in k order, from the f32 fragment image) + (b_ih + b_hh)[n], n in packed gate-row order.
+// Block = 64 tokens x 256 gate rows (the embedding rows in LDS), thread = one gate row.
+constexpr int FOLD_EV = 64;
+__global__ __launch_bounds__(256) void fold_emb_gates_kernel(const float* __restrict__ emb, const float* __restrict__ decw,
+                                                             const float* __restrict__ decb, int V,
+                                                             float* __restrict__ out) {
+  __shared__ float es[FOLD_EV][E];
+  const int v0 = blockIdx.x * FOLD_EV, n = blockIdx.y * 256 + threadIdx.x;
+  for (int i = threadIdx.x; i < FOLD_EV * E; i += 256) {
+    const int v = v0 + i / E;
+    es[i / E][i % E] = v < V ? emb[(size_t)v * E + i % E] : 0.f;
+  }
+  __syncthreads();
+  float acc[FOLD_EV];
+#pragma unroll
+  for (int j = 0; j < FOLD_EV; ++j) acc[j] = 0.f;
+  const int nt = n >> 4, rr = n & 15;
+  for (int k = 0; k < E; ++k) {
+    // pack_frag: block (nt, kc), [q][lane][4] with lane = row + 16 ((k % 64) / 16), q = (k % 16) / 4
+    const int kc = k >> 6, kk = k & 63;
+    const int lane = rr + 16 * (kk >> 4), q = (kk & 15) >> 2;
+    const float w = decw[((size_t)nt * (KDEC / 64) + kc) * FRAG + (q * 64 + lane) * 4 + (kk & 3)];
+#pragma unroll
+    for (int j = 0; j < FOLD_EV; ++j) acc[j] = fmaf(es[j][k], w, acc[j]);
+  }
+  const float b = decb[n];
+#pragma unroll
+  for (int j = 0; j < FOLD_EV; ++j)
+    if (v0 + j < V) out[(size_t)(v0 + j) * (4 * HD) + n] = acc[j] + b;
+}
+
+hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, hipStream_t s) {
+  const int VT = fold_vtiles(V);
+  if (VT > L.VP / 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(fold_image_kernel, dim3((VT + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w16,
+                     W + L.dec_w16, VT, wfold);
+  hipLaunchKernelGGL(fold_emb_gates_kernel, dim3((V + FOLD_EV - 1) / FOLD_EV, 4 * HD / 256), dim3(256), 0, s,
+                     W + L.emb, W + L.dec_w, W + L.dec_b, V, emb_gates);
+  return hipGetLastError();
+}
 
 // ------------------------------------------------------------------ init
 // st0[r] = [ctx 0 | h_fin(b) | c_fin(b)], tok = sos, src = r, score = 0 (model.py:531-535,
@@ -1609,6 +1720,17 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
   else launch_dg<4, 10, 3, 4, 2, true, 32, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
+// the folded step's GEMM (KB): 64 x 112 blocks (R <= 32: 32 x 112), ring of three 64-deep stages
+// (44 KB each); at R = 256, 4 x 63 = 252 blocks cover the 441 tiles (313 vocabulary + 128 gate)
+// in one round, 721 KB per block against 590 KB (projection) + 491 KB (LSTMCell) before
+template <class ASrc, class Epi>
+static void launch_fold_gemm(int R, int NB, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi,
+                             hipStream_t s) {
+  const int nkt = KPROJ / DG_BK;
+  if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+  else launch_dg<4, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+}
+
 // ------------------------------------------------------------------ host drivers
 // per-block row partials from the projection epilogue: the vocabulary must fit the 64 partial
 // blocks; beam search uses them at temperature 1 only (they are of x, not x / T)
@@ -1688,6 +1810,72 @@ void dg_trace_dump() {
   }
 }
 
+// the folded greedy step's GEMM (KB) on st_new = [ctx | h] of step l: partials of step l and, unless
+// l is the last step, the next step's gate pre-activations
+static void fold_gemm_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, hipStream_t s) {
+  const int R = a.B;
+  const int VT = fold_vtiles(a.V);
+  const bool gates = l + 1 < a.max_len;
+  const int ntiles = VT + FOLD_GT;
+  const int NB = gates ? (ntiles + FOLD_NT - 1) / FOLD_NT : (VT + FOLD_NT - 1) / FOLD_NT;
+  ProfScope ps(a.prof, CASR_K_PROJ, s);
+  ProjA asrc{d.st[(l + 1) & 1], R, 1};
+  GreedyPart gp = d.part;
+  gp.tmx = nullptr;
+  FoldEpi epi{a.W + a.L.proj_b, d.newdone, R, a.V, VT, l, total, d.err, gp, a.fb.gates};
+  launch_fold_gemm(R, NB, ntiles, a.fb.wfold, asrc, epi, s);
+}
+
+static int fold_col_blocks(int V) { return (fold_vtiles(V) + FOLD_NT - 1) / FOLD_NT; }
+
+// CASR_OPT_DEC_FOLD (casr_internal.h): step 0 as before (LSTMCell GEMM + attention from the query
+// partials), then the fused GEMM at every step and the cell inside the attention from step 1 on
+static hipError_t run_greedy_fold(const DecodeArgs& a, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
+                                  uint8_t* finished, float* accum, float* align, hipStream_t s) {
+  const int R = a.B;
+  const int nbp = fold_col_blocks(a.V);
+  if (nbp > GP_NB) return hipErrorInvalidValue;
+  const bool fuse = a.fuse_select != 0;
+  hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, 1, a.sos, d.tok[0],
+                     d.src[0], d.score[0], nullptr);
+  for (int l = 0; l < a.max_len; ++l) {
+    float* al = align ? align + (size_t)l * a.Tp * R : nullptr;
+    float* st_new = d.st[(l + 1) & 1];
+    hipError_t e;
+    if (l == 0) {
+      {
+        ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
+        DecLstmA asrc{a.W + a.L.emb16, d.st[0], d.tok[0], d.src[0], d.err, R, a.V, 1};
+        DecLstmEpi epi{a.W + a.L.dec_b, d.st[0], st_new, asrc, d.newdone, a.W + a.L.w_hidden, d.qpart, R, 0, R};
+        epi.hw = 1;
+        launch_dec_lstm(R, a.W + a.L.dec_w16, asrc, epi, 1, s);
+      }
+      ProfScope ps(a.prof, CASR_K_ATTENTION, s);
+      e = launch_attention_step(a, st_new, d.qpart, al, d.newdone, 0, R, s);
+    } else {
+      ProfScope ps(a.prof, CASR_K_ATTENTION, s);
+      AttnCell cell{};
+      cell.st_old = d.st[l & 1];
+      cell.gates = a.fb.gates;
+      cell.emb_gates = a.fb.emb_gates;
+      cell.w_hidden = a.W + a.L.w_hidden;
+      cell.tok = d.tok[l & 1];
+      cell.err = d.err;
+      cell.sel = fuse ? 1 : 0;
+      cell.gs = GreedySel{d.part, nbp, l - 1, a.max_len, a.eos, finished, out_len, accum, tokens, d.newdone};
+      e = launch_attention_cell_step(a, st_new, cell, al, d.newdone, l, R, s);
+    }
+    if (e != hipSuccess) return e;
+    fold_gemm_step(a, d, l, R, s);
+    if (fuse && l + 1 < a.max_len) continue;
+    ProfScope ps(a.prof, CASR_K_SELECT, s);
+    hipLaunchKernelGGL(greedy_select_part_kernel, dim3((R + 3) / 4), dim3(256), 0, s, d.part, nbp, a.V, R, l,
+                       a.max_len, a.eos, d.tok[(l + 1) & 1], d.src[(l + 1) & 1], finished, out_len, accum, tokens,
+                       d.newdone, d.err);
+  }
+  return hipGetLastError();
+}
+
 hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, int32_t* out_len,
                       uint8_t* finished, float* accum, float* align, hipStream_t s) {
   DecodeArgs a = a_in;
@@ -1702,6 +1890,7 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
   fl.add32(tokens, 0xffffffffu, (size_t)R * a.max_len);
   hipError_t e0 = fill_multi(fl, s);
   if (e0 != hipSuccess) return e0;
+  if (a.fold) return run_greedy_fold(a, d, tokens, out_len, finished, accum, align, s);
   // the select of step l runs inside step l+1's LSTMCell (GreedySel) when the projection writes
   // per-block partials; the last step's select is a launch of its own.  CASR_OPT_FUSE_SELECT = 0
   // keeps every select a launch (the same bits either way)

@@ -232,11 +232,20 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            them go to one launch of half tiles (default); 0: partial last round
  *   CASR_OPT_ATTN_KPB        beam rows per attention block at k > 2: 0 auto (8 at B >= 256 and
  *                            k >= 8, else 4), 4 or 8
- * One option selects a numerics variant instead (results within the attention tolerance, not bit
- * for bit; tests/test_gpu_parity.py compares the two):
+ * Two options select numerics variants instead (the same token ids, floating-point results within
+ * the stated tolerances, not bit for bit; tests/test_gpu_parity.py compares each pair):
  *   CASR_OPT_ATTN_DIRECT     0: attention scores in the split exponential form 1 - 2 / (1 + e^{2k}
  *                            e^{2q}) (default; one transcendental per term); 1: the
- *                            direct tanh(k + q) form the split form falls back to per block */
+ *                            direct tanh(k + q) form the split form falls back to per block
+ *   CASR_OPT_DEC_FOLD        1: greedy decode in two launches per step (s16x3; default): the
+ *                            projection GEMM also computes the next step's LSTM gate
+ *                            pre-activations from the same [ctx | h] rows, the embedding part of
+ *                            the gates is a per-token table built at bind, and the LSTM cell and
+ *                            the attention query run inside the attention kernel;
+ *                            0: three launches per step (LSTMCell GEMM, attention, projection).
+ *                            Replaces decoder.py:104-114 + attention.py:92 + decoder.py:129-135 per
+ *                            step with the same arithmetic regrouped (gates = [ctx | h] W_ch^T +
+ *                            (emb W_emb^T + b), q by f32 fma chains) */
 enum {
   CASR_OPT_FUSE_SELECT = 0,
   CASR_OPT_REC_LAYOUT = 1,
@@ -248,7 +257,8 @@ enum {
   CASR_OPT_GEMM16_TAIL = 7,
   CASR_OPT_ATTN_KPB = 8,
   CASR_OPT_ATTN_DIRECT = 9,
-  CASR_OPT_COUNT = 10
+  CASR_OPT_DEC_FOLD = 10,
+  CASR_OPT_COUNT = 11
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

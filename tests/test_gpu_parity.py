@@ -501,6 +501,44 @@ def test_attention_split_form_vs_direct(eng, name):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("name", ["plain", "peaked"])
+def test_decode_fold_vs_three_launches(eng, name):
+    """The folded greedy step (CASR_OPT_DEC_FOLD, default under s16x3: the projection GEMM also
+    computes the next step's LSTM gates from the same [ctx | h] rows, the embedding part of the gates
+    comes from the per-token table, the cell and q = h . W_hidden run inside the attention kernel)
+    against the three-launch step (LSTMCell GEMM, attention, projection): the same arithmetic
+    regrouped (decoder.py:104-114, attention.py:92, decoder.py:129-135), so identical tokens,
+    lengths and finished flags, scores within 2e-3 and alignments within 1e-5; on the golden batch
+    (ragged) and at the headline size (B = 256, T = 800, all 40 steps).  Under f32 the option has no
+    effect (the fold needs the s16 images): both runs take the three-launch step."""
+    def run(fold, **kw):
+        eng.set_option("DEC_FOLD", fold)
+        eng.profile(["dec_lstm"])
+        try:
+            g = eng.greedy(**kw)
+            n_lstm = eng.profile_read()["dec_lstm"][0]
+        finally:
+            eng.profile([])
+            eng.set_option("DEC_FOLD", 1)
+        assert eng.device_flags() == 0
+        return g, n_lstm
+
+    bind(eng, name)
+    for feat, flen in (golden_features(eng), _bench_batch(eng, 256)):
+        eng.encode(feat, flen)
+        align = feat.shape[0] < 64
+        f, n_f = run(1, alignment=align)
+        u, n_u = run(0, alignment=align)
+        # the fold runs the LSTMCell GEMM at step 0 only; the three-launch step at every step
+        assert n_u == CFG.max_len
+        assert n_f == (1 if eng.requested == "s16x3" else CFG.max_len)
+        for k in ("tokens", "out_len", "finished"):
+            assert torch.equal(f[k].cpu(), u[k].cpu()), k
+        np.testing.assert_allclose(f["accum"].cpu().numpy(), u["accum"].cpu().numpy(), atol=2e-3, rtol=0)
+        if align:
+            np.testing.assert_allclose(f["alignment"].cpu().numpy(), u["alignment"].cpu().numpy(), atol=1e-5, rtol=0)
+
+
 def test_bind_refuses_foreign_blob(eng):
     """A blob of another layout (size or stamp) is refused on bind, not read past its end."""
     from casr import lib as L
