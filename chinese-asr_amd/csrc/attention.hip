@@ -42,10 +42,11 @@ constexpr int AT_CELL_FLOATS = HD + AT_QS * A;
 
 // LDS: qs, eqs [AT_APAD][KPB] | vs, v2s [A] | (AT_MAXG unused) | scratch | es [Tq][KPB] | (CELL: h,
 // query slices) | value rows
-template <int KPB, bool CELL = false>
+// (CELL 2, the beam cell phase, keeps its h rows and query slices in the score scratch instead)
+template <int KPB, int CELL = 0>
 __host__ __device__ constexpr size_t attn_smem_floats(int Tp) {
   return (size_t)2 * KPB * AT_APAD + 2 * A + AT_MAXG + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp) +
-         (CELL ? AT_CELL_FLOATS : 0);
+         (CELL == 1 ? AT_CELL_FLOATS : 0);
 }
 
 // Split exponential form of the score tanh.  tanh(k + q) = 1 - 2 / (1 + e^{2k} e^{2q}): with
@@ -95,16 +96,19 @@ CASR_DEV f32x2 tanh_fast2(f32x2 x) {
 // diagnostics (CASR_DG_TRACE, tools/probes/dg_trace.py): per-block phase stamps of the last launch
 __device__ uint32_t* g_at_trace = nullptr;
 
-// CELL (the folded greedy step, casr_internal.h KA; KPB = 1, row r = b): before the attention the
-// block runs the select of step l - 1 for its row, the LSTM cell on gates_prev[r] + emb_gates[tok]
-// and q = h . W_hidden itself (no query partials); st receives h, c (and ctx as always).
-template <int KPB, bool CELL = false>
+// CELL (the folded step, casr_internal.h KA): before the attention the block runs the LSTM cell of
+// its rows on gates_prev + emb_gates[tok] and q = h . W_hidden itself (no query partials); st
+// receives h, c (and ctx as always).  CELL 1, greedy (KPB = 1, row r = b): the block first runs the
+// select of step l - 1 for its row.  CELL 2, beam (KPB = 4 or 8): tokens and predecessor rows come
+// from the beam select; gates_prev and c are read at the predecessor row.
+template <int KPB, int CELL = 0>
 __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float* __restrict__ st, const float* __restrict__ qpart, const float* __restrict__ keysT,
     const float* __restrict__ ekT, const float* __restrict__ enc, const int32_t* __restrict__ lens,
     const float* __restrict__ vv, int R, int k, int Tp, float* __restrict__ align, const int32_t* __restrict__ newdone,
     int l, int total, int npf, int direct, int nq, int V, AttnCell cell) {
-  static_assert(!CELL || KPB == 1, "the folded step is greedy: one row per block");
+  static_assert(CELL != 1 || KPB == 1, "the folded greedy step: one row per block");
+  static_assert(CELL != 2 || KPB >= 2, "the folded beam step: beam rows of one utterance per block");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   uint32_t* atr = g_at_trace ? g_at_trace + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int i) {
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   };
   stamp(0);
   // (CELL: the early exit is decided after the block's own select, below)
-  if (!CELL && done_before(newdone, l) >= total) return;
+  if (CELL != 1 && done_before(newdone, l) >= total) return;
   const int Tq = attn_tq(Tp);
   float* qs = sm;                   // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
   float* eqs = qs + KPB * AT_APAD;  // [AT_APAD][KPB]: exp(2q) (split form), zero past A
@@ -121,14 +125,14 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   float* xs = v2s + A + AT_MAXG;    // scratch
   float* es = xs + attn_scratch_floats<KPB>(Tq);  // [Tq][KPB]: one 4 x KPB-byte read per t
   float* hs = es + KPB * Tq;                       // CELL: [HD] h, then [AT_QS][A] query slices
-  float* vl = hs + (CELL ? AT_CELL_FLOATS : 0);    // [npf][C]: value rows 0..npf-1 (LDS-DMA)
+  float* vl = hs + (CELL == 1 ? AT_CELL_FLOATS : 0);  // [npf][C]: value rows 0..npf-1 (LDS-DMA)
   const int b = blockIdx.x, j0 = blockIdx.y * KPB;
   const int nk = min(KPB, k - j0);
   const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
   const int len = min(lens[b], Tp);
   const size_t row0 = (size_t)b * k + j0;
 
-  if constexpr (CELL) {
+  if constexpr (CELL == 1) {
     // 0. the folded step's LSTM cell (decoder.py:104-114) and query (attention.py:92) for row r.
     // W_hidden slice (rows 32 us .. +31, columns 4 a4 .. +3), the previous step's gate
     // pre-activations of unit u = tid and its c are loaded first: none depends on the select
@@ -147,6 +151,12 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     for (int g = 0; g < 4; ++g) gprev[g] = cell.gates[(size_t)r * (4 * HD) + gcol(g, u)];
     const float cold = cell.st_old[(size_t)r * ST + C + HD + u];
     if (wv == 0) {  // the select of step l - 1 (greedy_select_part_kernel's arithmetic) and its bookkeeping
+      // rows finished before step l - 1 (the select's own skip) and before step l (the block's early
+      // exit), from one load of the counters issued with the partials: the second misses what this
+      // launch's selects add to step l - 1, so a block that sees every row finished skips work nothing
+      // downstream reads, and one that does not computes it
+      int dn_sel, dn;
+      done_before2(newdone, cell.gs.lsel, l, dn_sel, dn);
       int t = 0;
       if (cell.sel) {
         const GreedySel& gs = cell.gs;
@@ -165,7 +175,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
           acc0 = gs.accum[r];
           len0 = gs.out_len[r];
         }
-        if (done_before(gs.newdone, gs.lsel) < total) {  // else nothing downstream runs any more
+        if (dn_sel < total) {  // else nothing downstream runs any more
           float gm = m;
           int gi = mi;
           wave_best(gm, gi);
@@ -185,9 +195,6 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
           t = 0;
         }
       }
-      // after this wave's own bookkeeping: rows finished before step l (a block that sees them all
-      // skips work nothing downstream reads; one that does not computes it)
-      const int dn = done_before(newdone, l);
       if (ln == 0) {
         tk_s = t;
         skip_s = dn >= total;
@@ -224,6 +231,76 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       qs[a] = q;
       eqs[a] = split_exp2x(q);
     }
+  }
+  if constexpr (CELL == 2) {
+    // 0. the folded beam step's LSTM cell for the block's nk rows r = row0 + j: token tok[r],
+    // predecessor s = src[r] (clamped and reported like DecLstmA::bind).  Thread = unit u; h rows
+    // [KPB][HD] and the query slices [AT_THREADS / A][KPB][A] in the score scratch (free until the
+    // scores).  q: thread (column a, slice us of 128 units), an f32 fma chain per row in unit
+    // order, the slices added in slice order.
+    float* hsb = xs;
+    float* qsl = xs + KPB * HD;
+    constexpr int NS = AT_THREADS / A, UPS = HD / NS;
+    const int a = tid & (A - 1), us = tid / A;
+    const int u = tid;
+    auto gcol = [](int g, int u) { return (u >> 4) * 64 + g * 16 + (u & 15); };  // packed_gate_row
+    int sr[KPB], tk[KPB], bad = 0;
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) {
+      const int r = (int)row0 + min(j, nk - 1);
+      int sj = cell.src[r], tj = cell.tok[r];
+      bad |= (unsigned)sj >= (unsigned)R ? CASR_DEV_BAD_SRC : 0;
+      bad |= (unsigned)tj >= (unsigned)V ? CASR_DEV_BAD_TOKEN : 0;
+      sr[j] = (unsigned)sj < (unsigned)R ? sj : r;
+      tk[j] = (unsigned)tj < (unsigned)V ? tj : 0;
+    }
+    if (bad && tid == 0) atomicOr(cell.err, bad);
+    float gp[KPB][4], eg[KPB][4], co[KPB];
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        gp[j][g] = cell.gates[(size_t)sr[j] * (4 * HD) + gcol(g, u)];
+        eg[j][g] = cell.emb_gates[(size_t)tk[j] * (4 * HD) + gcol(g, u)];
+      }
+      co[j] = cell.st_old[(size_t)sr[j] * ST + C + HD + u];
+    }
+    float whs[UPS];  // W_hidden[UPS us + i][a], in flight under the cells
+#pragma unroll
+    for (int i = 0; i < UPS; ++i) whs[i] = cell.w_hidden[(size_t)(UPS * us + i) * A + a];
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) {
+      float h2 = 0.f, c2;
+      if (j < nk) {
+        const size_t r = row0 + j;
+        lstm_cell_hw(gp[j][0] + eg[j][0], gp[j][1] + eg[j][1], gp[j][2] + eg[j][2], gp[j][3] + eg[j][3], co[j], h2,
+                     c2);
+        st[r * ST + C + u] = h2;
+        st[r * ST + C + HD + u] = c2;
+        reinterpret_cast<uint32_t*>(st)[r * ST + ST16 + C + u] = split16_word(h2);
+      }
+      hsb[j * HD + u] = h2;
+    }
+    __syncthreads();
+    float qa[KPB];
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) qa[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < UPS; ++i)
+#pragma unroll
+      for (int j = 0; j < KPB; ++j) qa[j] = fmaf(hsb[j * HD + UPS * us + i], whs[i], qa[j]);
+#pragma unroll
+    for (int j = 0; j < KPB; ++j) qsl[(us * KPB + j) * A + a] = qa[j];
+    __syncthreads();
+    for (int f = tid; f < KPB * A; f += AT_THREADS) {
+      const int j = f / A, c = f - j * A;
+      float q = qsl[j * A + c];
+#pragma unroll
+      for (int i = 1; i < NS; ++i) q += qsl[(i * KPB + j) * A + c];
+      qs[c * KPB + j] = j < nk ? q : 0.f;
+      eqs[c * KPB + j] = j < nk ? split_exp2x(q) : 0.f;
+    }
+    __syncthreads();  // the score phase overwrites the scratch
   }
   // 1. q = sum of the HD/16 partials in partial order (p = 0, 1, ...), v -> LDS.  The block's
   // KPB rows are consecutive, so partial p of all of them is one contiguous KPB x A span: a thread
@@ -586,7 +663,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 // budget (two blocks per CU) unchanged; the knob was removed in round 3.
 static size_t attn_lds_budget() { return (size_t)156 * 1024; }
 
-template <int KPB, bool CELL = false>
+template <int KPB, int CELL = 0>
 static int attn_npf(int Tp) {
   const size_t fixed = attn_smem_floats<KPB, CELL>(Tp) * sizeof(float);
   const size_t budget = attn_lds_budget();
@@ -595,7 +672,7 @@ static int attn_npf(int Tp) {
   return rows < Tp ? rows : (Tp + 3) & ~3;
 }
 
-template <int KPB, bool CELL = false>
+template <int KPB, int CELL = 0>
 static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart, float* align, int32_t* newdone,
                              int l, int total, hipStream_t s, const AttnCell& cell = AttnCell{}) {
   const int npf = attn_npf<KPB, CELL>(a.Tp);
@@ -617,8 +694,12 @@ static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart,
 
 hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const AttnCell& cell, float* align,
                                       int32_t* newdone, int l, int total, hipStream_t s) {
-  if (a.k != 1) return hipErrorInvalidValue;  // greedy only
-  return launch_kpb<1, true>(a, st, nullptr, align, newdone, l, total, s, cell);
+  if (a.k == 1) return launch_kpb<1, 1>(a, st, nullptr, align, newdone, l, total, s, cell);
+  switch (attention_kpb(a.B, a.k, a.attn_kpb)) {
+    case 4: return launch_kpb<4, 2>(a, st, nullptr, align, newdone, l, total, s, cell);
+    case 8: return launch_kpb<8, 2>(a, st, nullptr, align, newdone, l, total, s, cell);
+    default: return hipErrorInvalidValue;  // the folded beam step needs 4 or 8 rows per block
+  }
 }
 
 // beam rows per block at k > 2 (CASR_OPT_ATTN_KPB, 0 = auto).  4 rows per block at B < 256: 8 rows

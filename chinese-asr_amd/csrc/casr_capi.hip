@@ -173,6 +173,7 @@ struct casr_handle {
   int precision = CASR_PREC_S16X3;  // requested (casr_set_precision)
   bool s16_valid = false;           // the bound blob's s16 images are usable (Layout::info)
   bool proj_small = false;          // every |W_p| < 16 (Layout::info + 4)
+  bool dec_small = false;           // every decoder LSTM weight < 16 (Layout::info + 5)
   DevBuf x16;                       // s16 row image of the current layer input [B*Tp][Kp]
   // folded greedy decode (CASR_OPT_DEC_FOLD): fused projection | LSTM-gate fragment image and the
   // per-token gate table, built at bind from an s16-valid blob; the gates buffer [R][4 HD]
@@ -342,6 +343,12 @@ int casr_pack_weights(const casr_config* cfg, const casr_weights_host* w, float*
   // info word 4: every projection weight below 16 in magnitude, so w_hi 2^11 is an f16 and the
   // beam projection can run its one-accumulator s16x3 form (decoder.hip dgemm_kernel ONE)
   out[L.info + 4] = (w->proj_w && in_range(w->proj_w, (size_t)cfg->vocab * KPROJ, 16.f)) ? 1.f : 0.f;
+  // info word 5: every decoder LSTM weight below 16 in magnitude: with word 4 the folded beam step's
+  // fused GEMM (projection | LSTM gates) can run the one-accumulator form (decoder.hip FoldEpi)
+  out[L.info + 5] = (w->dec_w_ih && w->dec_w_hh && in_range(w->dec_w_ih, (size_t)4 * HD * (E + C), 16.f) &&
+                     in_range(w->dec_w_hh, (size_t)4 * HD * HD, 16.f))
+                        ? 1.f
+                        : 0.f;
   // layout stamp: casr_bind_weights refuses a blob packed by a build with another layout
   const uint32_t stamp[3] = {LAYOUT_MAGIC, (uint32_t)(L.total & 0xFFFFFFFFu), (uint32_t)(L.total >> 32)};
   std::memcpy(out + L.info + 1, stamp, sizeof stamp);
@@ -436,7 +443,7 @@ int casr_create(const casr_config* cfg, int device, casr_handle** out) {
 int casr_bind_weights(casr_handle* h, const float* packed_device) {
   if (!h || !packed_device) return fail(h, CASR_ERR_ARG, "handle/weights NULL");
   HIP_OK(h, hipSetDevice(h->device));
-  float info[5] = {};
+  float info[6] = {};
   HIP_OK(h, hipMemcpy(info, packed_device + h->L.info, sizeof info, hipMemcpyDeviceToHost));
   uint32_t stamp[3];
   std::memcpy(stamp, info + 1, sizeof stamp);
@@ -447,6 +454,7 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
                 "expected %08x, %zu floats)", stamp[0], stamp[1], LAYOUT_MAGIC, h->L.total);
   h->s16_valid = info[0] == 1.f;
   h->proj_small = info[4] == 1.f;
+  h->dec_small = info[5] == 1.f;
   h->W = packed_device;
   h->graphs.clear();  // captured graphs bake in the precision and weight pointers
   // the folded greedy step's tables (decoder.hip build_fold): derived from this blob, so rebuilt
@@ -894,8 +902,12 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   a.attn_kpb = h->tune[CASR_OPT_ATTN_KPB];
   a.attn_direct = h->tune[CASR_OPT_ATTN_DIRECT];
   a.proj_small = h->proj_small;
-  // the folded greedy step (greedy only: casr_greedy passes k = 1; run_beam ignores it)
-  a.fold = k == 1 && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
+  // the folded step: greedy (casr_greedy passes k = 1), or beam at R >= 1024 rows with 4 or 8 beam
+  // rows per attention block and every projection / LSTM weight < 16 (the fused GEMM's
+  // one-accumulator beam shapes, decoder.hip launch_fold_gemm)
+  const bool fold_beam = k > 1 && R >= 1024 && h->proj_small && h->dec_small &&
+                         attention_kpb(B, k, h->tune[CASR_OPT_ATTN_KPB]) >= 4;
+  a.fold = (k == 1 || fold_beam) && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
   if (a.fold) {
     HIP_OK(h, h->fgates.ensure((size_t)R * 4 * HD * sizeof(float)));
     a.fb = FoldBufs{h->wfold.as<float>(), h->egates.as<float>(), h->fgates.as<float>()};
@@ -971,7 +983,7 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
   uint32_t lmw, lw;
   std::memcpy(&lmw, &lm_weight, 4);
   std::memcpy(&lw, &length_weight, 4);
-  const std::vector<uint64_t> key = {3, (uint64_t)a.s16, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
+  const std::vector<uint64_t> key = {3, (uint64_t)a.s16, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)a.fold, (uint64_t)h->fgates.p, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)k, lmw, lw, (uint64_t)h->W,
                                      (uint64_t)h->gout.p, (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->bp.p, (uint64_t)h->tk.p, (uint64_t)h->rec.p,
                                      (uint64_t)h->enc_out, (uint64_t)h->keysT.p, (uint64_t)h->hfin.p,

@@ -183,6 +183,24 @@ CASR_DEV int done_before(const int32_t* __restrict__ newdone, int l) {
          (__builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48));
 }
 
+// rows finished before steps l1 and l2 from one pass of loads over the counters
+CASR_DEV void done_before2(const int32_t* __restrict__ newdone, int l1, int l2, int& d1, int& d2) {
+  const int lane = threadIdx.x & 63, lm = max(l1, l2);
+  int s1 = 0, s2 = 0;
+  for (int i0 = 0; i0 < lm; i0 += 64) {
+    const int i = i0 + lane;
+    const int v = i < lm ? newdone[i] : 0;
+    s1 += i < l1 ? v : 0;
+    s2 += i < l2 ? v : 0;
+  }
+  s1 = row16_isum(s1);
+  s2 = row16_isum(s2);
+  d1 = (__builtin_amdgcn_readlane(s1, 0) + __builtin_amdgcn_readlane(s1, 16)) +
+       (__builtin_amdgcn_readlane(s1, 32) + __builtin_amdgcn_readlane(s1, 48));
+  d2 = (__builtin_amdgcn_readlane(s2, 0) + __builtin_amdgcn_readlane(s2, 16)) +
+       (__builtin_amdgcn_readlane(s2, 32) + __builtin_amdgcn_readlane(s2, 48));
+}
+
 // Hardware-exp forms (v_exp_f32 / v_rcp_f32, no IEEE division: __frcp_rn / __fdividef / 1.f / x
 // compile to a div_scale / div_fmas / div_fixup sequence of ~10 dependent instructions, and this
 // cell sits on the recurrence's critical path).  exp(y) = exp2(y log2 e) with the product rounded

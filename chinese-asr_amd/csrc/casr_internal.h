@@ -369,14 +369,16 @@ inline bool dec_wide(int R) { return R >= 2048; }
 inline int dec_q_slots(int R) { return dec_wide(R) ? HD / 32 : HD / 16; }
 hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qpart, float* align,
                                  int32_t* newdone, int l, int total, hipStream_t s);
-// the folded step's attention (KA above): st_old supplies c, st receives h, c and ctx; sel: the
-// fused select of step gs.lsel (else tokens from tok)
+// the folded step's attention (KA above): st_old supplies c, st receives h, c and ctx.  Greedy
+// (k = 1): sel = the fused select of step gs.lsel (else tokens from tok).  Beam (k > 1, 4 or 8 rows
+// per block): tokens and predecessor rows from the beam select (tok, src)
 struct AttnCell {
   const float* st_old;
   const float* gates;
   const float* emb_gates;
   const float* w_hidden;  // [HD][A]
-  const int32_t* tok;     // sel == 0
+  const int32_t* tok;     // sel == 0 (beam: the select's tokens of the block's rows)
+  const int32_t* src;     // beam: the predecessor row of each row (gates_prev and c are read there)
   int32_t* err;
   int sel;
   GreedySel gs;

@@ -313,10 +313,13 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   // stages: a skipped block leaves no DMA behind)
   auto erow0 = [&](int rs) { return rb * BM + (ws * RS + rs) * 16 + 4 * (lane >> 4); };
   const int nbw = nb * WC + wc;  // the wave's column block in units of NTW tiles (the epilogue's nb)
-  typename Epi::Pre pre[RS];
+  // (an epilogue whose prefetched operands do not depend on the rows (kPreRowFree: the column biases)
+  // loads them once for all RS slabs: registers the 256-row blocks need for their accumulators)
+  constexpr int NPRE = Epi::kPreRowFree ? 1 : RS;
+  typename Epi::Pre pre[NPRE];
   if (kq == 0)
 #pragma unroll
-    for (int rs = 0; rs < RS; ++rs) epi.template prefetch<NTW>(pre[rs], erow0(rs), nbw, lane & 15, bad);
+    for (int rs = 0; rs < NPRE; ++rs) epi.template prefetch<NTW>(pre[rs], erow0(rs), nbw, lane & 15, bad);
   if (epi.skip()) return;
   if (bad) atomicOr(epi.err_flags(), bad);
   stamp(1);
@@ -345,7 +348,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   stamp(3);
   if (kq == 0)
 #pragma unroll
-    for (int rs = 0; rs < RS; ++rs) epi.template late<NTW>(pre[rs], erow0(rs), nbw, lane & 15);  // under the k-slice exchange
+    for (int rs = 0; rs < NPRE; ++rs) epi.template late<NTW>(pre[rs], erow0(rs), nbw, lane & 15);  // under the k-slice exchange
   if constexpr (S16) {
 #pragma unroll
     for (int rs = 0; rs < RS; ++rs)
@@ -392,7 +395,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   const int ew = ws * WC + wc;
   float* escr = (ew < 4 ? lb1 : lb0) + (ew & 3) * 16 * (16 * NTW + 4);
 #pragma unroll
-  for (int rs = 0; rs < RS; ++rs) epi.template run<NTW>(acc[rs], erow0(rs), nbw, r, pre[rs], escr);
+  for (int rs = 0; rs < RS; ++rs) epi.template run<NTW>(acc[rs], erow0(rs), nbw, r, pre[NPRE == 1 ? 0 : rs], escr);
   stamp(4);
 }
 
@@ -514,6 +517,7 @@ struct DecLstmA {
 
 struct DecLstmEpi {
   static constexpr int kTraceClass = 0;
+  static constexpr bool kPreRowFree = false;  // predecessor rows and c per row slab
   static constexpr bool kScratch = false;  // the epilogue's LDS: its own h tiles (ht), no slab
   const float* bias;  // packed [4HD]
   const float* st_old;
@@ -638,8 +642,96 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
 // exp(x - max)) and writes that partial (GreedyPart); greedy_select_part_kernel combines the
 // 64 partials of a row.  Beam search keeps the full logits (logits != nullptr).
 
+// Projection epilogue pieces (ProjEpi, FoldEpi).  Lane (g, u) holds rows row0 + e (e = 0..3) of
+// column tiles nb * NTN + tn, column 16 (nb NTN + tn) + u; bn: the columns' biases.
+// Beam logits: the wave's 16 rows x 16 NTN columns go through its LDS slab (row stride padded by 4
+// floats: the four row groups of a column write hit different banks), then out as float4 row
+// segments (one instruction covers 64 consecutive float4 of the tile, row-major: up to 640
+// contiguous bytes per row), and each 16-column tile's maximum (tmx, for the beam select's
+// threshold and candidate tiles; tiles < ntl only) is reduced over the quad of lanes that hold it.
+template <int NTN>
+__device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const float (&bn)[16], int row0, int nb,
+                                                int u, float* scr, float* logits, float* tmx, int R, int V,
+                                                int ntl) {
+  constexpr int RWS = 16 * NTN + 4, CH = 4 * NTN;  // slab row stride; float4 per tile row
+  const int lane = threadIdx.x & 63, g = lane >> 4;
+#pragma unroll
+  for (int tn = 0; tn < NTN; ++tn)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) scr[(4 * g + e) * RWS + tn * 16 + u] = acc[tn][e] + bn[tn];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const int rb0 = row0 - 4 * g, c0 = nb * 16 * NTN;
+  const bool vec = (V & 3) == 0;
+#pragma unroll
+  for (int i = 0; i < CH / 4; ++i) {
+    const int f = i * 64 + lane, rr = f / CH, ch = f - rr * CH;
+    const float4 v = *reinterpret_cast<const float4*>(scr + rr * RWS + 4 * ch);
+    const int row = rb0 + rr, col = c0 + 4 * ch;
+    if (row < R) {
+      float* dst = logits + (size_t)row * V + col;
+      if (vec && col + 3 < V) {
+        *reinterpret_cast<float4*>(dst) = v;
+      } else {
+        if (col < V) dst[0] = v.x;
+        if (col + 1 < V) dst[1] = v.y;
+        if (col + 2 < V) dst[2] = v.z;
+        if (col + 3 < V) dst[3] = v.w;
+      }
+    }
+    if (tmx) {
+      float m = fmaxf(fmaxf(col < V ? v.x : -INFINITY, col + 1 < V ? v.y : -INFINITY),
+                      fmaxf(col + 2 < V ? v.z : -INFINITY, col + 3 < V ? v.w : -INFINITY));
+      m = fmaxf(m, dpp_f<DPP_XOR1>(m));
+      m = fmaxf(m, dpp_f<DPP_XOR2>(m));
+      if ((lane & 3) == 0 && row < R && (col >> 4) < ntl) tmx[(size_t)row * GP_NT + (col >> 4)] = m;
+    }
+  }
+}
+
+// per-row partials over the block's columns n < V (greedy, and beam at temperature 1): lane (g, u)
+// holds columns 16 (nb NTN + tn) + u; the 16 lanes of one g share the rows
+template <int NTN>
+__device__ __forceinline__ void proj_row_partials(const f32x4 (&acc)[NTN], const float (&bn)[16], int row0, int nb,
+                                                  int u, const GreedyPart& gp, int R, int V) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float x[NTN];
+    float m = -INFINITY;
+    int mi = 0x7fffffff;
+#pragma unroll
+    for (int tn = 0; tn < NTN; ++tn) {
+      const int n = (nb * NTN + tn) * 16 + u;
+      x[tn] = acc[tn][e] + bn[tn];
+      if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
+        m = x[tn];
+        mi = n;
+      }
+    }
+    {  // the row's (max, lowest column among equal maxima) over the 16 lanes of this g
+      const float rm = row16_max(m);
+      mi = row16_min(m == rm ? mi : 0x7fffffff);
+      m = rm;
+    }
+    float sx = 0.f;
+#pragma unroll
+    for (int tn = 0; tn < NTN; ++tn) {
+      const int n = (nb * NTN + tn) * 16 + u;
+      if (n < V) sx += expf(x[tn] - m);
+    }
+    sx = row16_sum(sx);  // lane u == 0 (the row's first quad) writes it
+    const int row = row0 + e;
+    if (u == 0 && row < R) {
+      gp.mx[(size_t)row * GP_NB + nb] = m;
+      gp.se[(size_t)row * GP_NB + nb] = sx;
+      gp.ix[(size_t)row * GP_NB + nb] = mi;
+    }
+  }
+}
+
 struct ProjEpi {
   static constexpr int kTraceClass = 1;
+  static constexpr bool kPreRowFree = true;  // the column biases
   static constexpr bool kScratch = true;  // beam logits go out through per-wave LDS slabs
   const float* bias;
   float* logits;  // [R][V] (beam); nullptr in greedy mode
@@ -669,83 +761,8 @@ struct ProjEpi {
   __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p,
                                       float* scr) const {
     static_assert(NTN <= 16, "bias prefetch slots");
-    if (logits) {
-      // beam: the wave's 16 rows x 16 NTN columns go through its LDS slab (row stride padded by 4
-      // floats: the four row groups of a column write hit different banks), then out as float4
-      // row segments (one instruction covers 64 consecutive float4 of the tile, row-major: up to
-      // 640 contiguous bytes per row), and each 16-column tile's maximum (gp.tmx, for the
-      // select's threshold and candidate tiles) is reduced over the quad of lanes that hold it
-      constexpr int RWS = 16 * NTN + 4, CH = 4 * NTN;  // slab row stride; float4 per tile row
-      const int lane = threadIdx.x & 63, g = lane >> 4;
-#pragma unroll
-      for (int tn = 0; tn < NTN; ++tn)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) scr[(4 * g + e) * RWS + tn * 16 + u] = acc[tn][e] + p.bn[tn];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_wave_barrier();
-      const int rb0 = row0 - 4 * g, c0 = nb * 16 * NTN;
-      const bool vec = (V & 3) == 0;
-#pragma unroll
-      for (int i = 0; i < CH / 4; ++i) {
-        const int f = i * 64 + lane, rr = f / CH, ch = f - rr * CH;
-        const float4 v = *reinterpret_cast<const float4*>(scr + rr * RWS + 4 * ch);
-        const int row = rb0 + rr, col = c0 + 4 * ch;
-        if (row < R) {
-          float* dst = logits + (size_t)row * V + col;
-          if (vec && col + 3 < V) {
-            *reinterpret_cast<float4*>(dst) = v;
-          } else {
-            if (col < V) dst[0] = v.x;
-            if (col + 1 < V) dst[1] = v.y;
-            if (col + 2 < V) dst[2] = v.z;
-            if (col + 3 < V) dst[3] = v.w;
-          }
-        }
-        if (gp.tmx) {
-          float m = fmaxf(fmaxf(col < V ? v.x : -INFINITY, col + 1 < V ? v.y : -INFINITY),
-                          fmaxf(col + 2 < V ? v.z : -INFINITY, col + 3 < V ? v.w : -INFINITY));
-          m = fmaxf(m, dpp_f<DPP_XOR1>(m));
-          m = fmaxf(m, dpp_f<DPP_XOR2>(m));
-          if ((lane & 3) == 0 && row < R) gp.tmx[(size_t)row * GP_NT + (col >> 4)] = m;
-        }
-      }
-    }
-    if (!gp.mx) return;
-    // greedy partials of rows row0 + e over this block's columns: lane (g, u) holds columns
-    // (nb*5 + tn)*16 + u; the 16 lanes of one g share the rows
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float x[NTN];
-      float m = -INFINITY;
-      int mi = 0x7fffffff;
-#pragma unroll
-      for (int tn = 0; tn < NTN; ++tn) {
-        const int n = (nb * NTN + tn) * 16 + u;
-        x[tn] = acc[tn][e] + p.bn[tn];
-        if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
-          m = x[tn];
-          mi = n;
-        }
-      }
-      {  // the row's (max, lowest column among equal maxima) over the 16 lanes of this g
-        const float rm = row16_max(m);
-        mi = row16_min(m == rm ? mi : 0x7fffffff);
-        m = rm;
-      }
-      float sx = 0.f;
-#pragma unroll
-      for (int tn = 0; tn < NTN; ++tn) {
-        const int n = (nb * NTN + tn) * 16 + u;
-        if (n < V) sx += expf(x[tn] - m);
-      }
-      sx = row16_sum(sx);  // lane u == 0 (the row's first quad) writes it
-      const int row = row0 + e;
-      if (u == 0 && row < R) {
-        gp.mx[(size_t)row * GP_NB + nb] = m;
-        gp.se[(size_t)row * GP_NB + nb] = sx;
-        gp.ix[(size_t)row * GP_NB + nb] = mi;
-      }
-    }
+    if (logits) proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, GP_NT);
+    if (gp.mx) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
   }
 };
 
@@ -756,13 +773,15 @@ struct ProjEpi {
 // whose tiles are all gate tiles writes no partial; nbp = ceil(VT / NT) blocks do.
 struct FoldEpi {
   static constexpr int kTraceClass = 1;
-  static constexpr bool kScratch = false;
+  static constexpr bool kPreRowFree = true;  // the column biases
+  static constexpr bool kScratch = true;  // beam logits go out through per-wave LDS slabs
   const float* bias;  // proj_b [VP]
   const int32_t* newdone;
   int R, V, VT, l, total;
   int32_t* err;
-  GreedyPart gp;
-  float* gates;  // [R][4 HD]
+  GreedyPart gp;   // row partials (greedy; beam at temperature 1) or gp.mx == nullptr
+  float* gates;    // [R][4 HD]
+  float* logits;   // [R][V] (beam), or nullptr
   struct Pre {
     float bn[16];
   };
@@ -780,7 +799,8 @@ struct FoldEpi {
   template <int NTN>
   __device__ __forceinline__ void late(Pre&, int, int, int) const {}
   template <int NTN>
-  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p, float*) const {
+  __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p,
+                                      float* scr) const {
 #pragma unroll
     for (int tn = 0; tn < NTN; ++tn) {
       const int gt = nb * NTN + tn - VT;
@@ -792,39 +812,8 @@ struct FoldEpi {
       }
     }
     if (nb * NTN >= VT) return;  // no vocabulary tile in this block
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float x[NTN];
-      float m = -INFINITY;
-      int mi = 0x7fffffff;
-#pragma unroll
-      for (int tn = 0; tn < NTN; ++tn) {
-        const int n = (nb * NTN + tn) * 16 + u;
-        x[tn] = acc[tn][e] + p.bn[tn];
-        if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
-          m = x[tn];
-          mi = n;
-        }
-      }
-      {
-        const float rm = row16_max(m);
-        mi = row16_min(m == rm ? mi : 0x7fffffff);
-        m = rm;
-      }
-      float sx = 0.f;
-#pragma unroll
-      for (int tn = 0; tn < NTN; ++tn) {
-        const int n = (nb * NTN + tn) * 16 + u;
-        if (n < V) sx += expf(x[tn] - m);
-      }
-      sx = row16_sum(sx);
-      const int row = row0 + e;
-      if (u == 0 && row < R) {
-        gp.mx[(size_t)row * GP_NB + nb] = m;
-        gp.se[(size_t)row * GP_NB + nb] = sx;
-        gp.ix[(size_t)row * GP_NB + nb] = mi;
-      }
-    }
+    if (logits) proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, VT);
+    if (gp.mx) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
   }
 };
 
@@ -1720,21 +1709,35 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
   else launch_dg<4, 10, 3, 4, 2, true, 32, true>((ntiles + 9) / 10, R, ntiles, nkt, Wf, asrc, epi, s16, s);
 }
 
-// the folded step's GEMM (KB): 64 x 112 blocks (R <= 32: 32 x 112), ring of three 64-deep stages
-// (44 KB each); at R = 256, 4 x 63 = 252 blocks cover the 441 tiles (313 vocabulary + 128 gate)
-// in one round, 721 KB per block against 590 KB (projection) + 491 KB (LSTMCell) before
+// the folded step's GEMM (KB) over the 441 tiles (313 vocabulary + 128 gate) of the fused image.
+// Greedy: 64 x 112 blocks (R <= 32: 32 x 112), ring of three 64-deep stages (44 KB each); at R = 256,
+// 4 x 63 = 252 blocks in one round, 721 KB per block against 590 KB (projection) + 491 KB
+// (LSTMCell) for the three-launch step.  Beam (one-accumulator s16x3, 32-deep stages, wave tiles of
+// 16 RS rows x 112 columns, the 7-tile column blocks of the greedy shapes): 256 x 224 blocks, ring
+// of two 60 KB stages, at R >= 2048 (8 x 32 = 256 blocks at R = 2048, 1.97 MB each against 1.7 MB
+// + 1.3 MB); 128 x 224, ring of three, below (R = 1024: 256 blocks)
+constexpr int FOLD_NT_BEAM = 2 * FOLD_NT;
 template <class ASrc, class Epi>
-static void launch_fold_gemm(int R, int NB, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi,
+static void launch_fold_gemm(int R, bool beam, int NB, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi,
                              hipStream_t s) {
   const int nkt = KPROJ / DG_BK;
-  if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
-  else launch_dg<4, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+  if (!beam) {
+    if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+    else launch_dg<4, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+  } else if (dec_wide(R)) {
+    launch_dg<4, FOLD_NT_BEAM, 2, 4, 2, true, 32, true>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+  } else {
+    launch_dg<4, FOLD_NT_BEAM, 3, 2, 2, true, 32, true>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+  }
 }
 
 // ------------------------------------------------------------------ host drivers
 // per-block row partials from the projection epilogue: the vocabulary must fit the 64 partial
 // blocks; beam search uses them at temperature 1 only (they are of x, not x / T)
+static int fold_col_blocks(int V) { return (fold_vtiles(V) + FOLD_NT - 1) / FOLD_NT; }
 static int proj_col_blocks(const DecodeArgs& a) {
+  // the folded step's partials: one per 7-tile wave column in every shape
+  if (a.fold) return fold_col_blocks(a.V);
   const int nt = a.L.VP / 16, R = a.B * a.k;
   // the column block of a wave (ProjEpi's partial index): 5 tiles in every launch_proj shape (the
   // beam blocks' two wave columns), so the select's partial sums do not depend on R
@@ -1745,8 +1748,9 @@ static bool row_partials(const DecodeArgs& a) {
   return proj_col_blocks(a) <= GP_NB && (a.greedy_run || a.temperature == 1.0f);
 }
 
+// proj = false: LSTMCell and attention only (the folded step's step 0: its GEMM follows)
 static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
-                              hipStream_t s, const GreedySel* gsel = nullptr) {
+                              hipStream_t s, const GreedySel* gsel = nullptr, bool proj = true) {
   const int R = a.B * a.k;
   const float* st_old = d.st[l & 1];
   float* st_new = d.st[(l + 1) & 1];
@@ -1767,7 +1771,7 @@ static hipError_t decode_step(const DecodeArgs& a, DecodeBufs& d, int l, int tot
     e = launch_attention_step(a, st_new, d.qpart, align, d.newdone, l, total, s);
   }
   if (e != hipSuccess) return e;
-  {
+  if (proj) {
     ProfScope ps(a.prof, CASR_K_PROJ, s);
     ProjA asrc{st_new, R, a.s16};
     // greedy: per-block partials instead of logits; beam at temperature 1: logits and partials
@@ -1812,21 +1816,39 @@ void dg_trace_dump() {
 
 // the folded greedy step's GEMM (KB) on st_new = [ctx | h] of step l: partials of step l and, unless
 // l is the last step, the next step's gate pre-activations
+// beam: logits, and at temperature 1 the row partials and tile maxima, as decode_step's projection
 static void fold_gemm_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, hipStream_t s) {
-  const int R = a.B;
-  const int VT = fold_vtiles(a.V);
+  const int R = a.B * a.k;
+  const bool beam = !a.greedy_run;
+  const int VT = fold_vtiles(a.V), NT = beam ? FOLD_NT_BEAM : FOLD_NT;
   const bool gates = l + 1 < a.max_len;
   const int ntiles = VT + FOLD_GT;
-  const int NB = gates ? (ntiles + FOLD_NT - 1) / FOLD_NT : (VT + FOLD_NT - 1) / FOLD_NT;
+  const int NB = ((gates ? ntiles : VT) + NT - 1) / NT;
   ProfScope ps(a.prof, CASR_K_PROJ, s);
   ProjA asrc{d.st[(l + 1) & 1], R, 1};
-  GreedyPart gp = d.part;
-  gp.tmx = nullptr;
-  FoldEpi epi{a.W + a.L.proj_b, d.newdone, R, a.V, VT, l, total, d.err, gp, a.fb.gates};
-  launch_fold_gemm(R, NB, ntiles, a.fb.wfold, asrc, epi, s);
+  GreedyPart gp = row_partials(a) ? d.part : GreedyPart{nullptr, nullptr, nullptr, nullptr};
+  if (!beam || a.V > 16 * GP_NT) gp.tmx = nullptr;  // tile maxima: beam only
+  FoldEpi epi{a.W + a.L.proj_b, d.newdone, R, a.V, VT, l, total, d.err, gp, a.fb.gates, beam ? d.logits : nullptr};
+  launch_fold_gemm(R, beam, NB, ntiles, a.fb.wfold, asrc, epi, s);
 }
 
-static int fold_col_blocks(int V) { return (fold_vtiles(V) + FOLD_NT - 1) / FOLD_NT; }
+// the folded step's attention with its cell prologue (steps l >= 1): greedy with the fused select
+// of step l - 1 (sel), beam with the beam select's tokens and predecessor rows
+static hipError_t fold_attention_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
+                                      bool sel, const GreedySel& gs, hipStream_t s) {
+  ProfScope ps(a.prof, CASR_K_ATTENTION, s);
+  AttnCell cell{};
+  cell.st_old = d.st[l & 1];
+  cell.gates = a.fb.gates;
+  cell.emb_gates = a.fb.emb_gates;
+  cell.w_hidden = a.W + a.L.w_hidden;
+  cell.tok = d.tok[l & 1];
+  cell.src = d.src[l & 1];
+  cell.err = d.err;
+  cell.sel = sel ? 1 : 0;
+  cell.gs = gs;
+  return launch_attention_cell_step(a, d.st[(l + 1) & 1], cell, align, d.newdone, l, total, s);
+}
 
 // CASR_OPT_DEC_FOLD (casr_internal.h): step 0 as before (LSTMCell GEMM + attention from the query
 // partials), then the fused GEMM at every step and the cell inside the attention from step 1 on
@@ -1840,31 +1862,9 @@ static hipError_t run_greedy_fold(const DecodeArgs& a, DecodeBufs& d, int32_t* t
                      d.src[0], d.score[0], nullptr);
   for (int l = 0; l < a.max_len; ++l) {
     float* al = align ? align + (size_t)l * a.Tp * R : nullptr;
-    float* st_new = d.st[(l + 1) & 1];
-    hipError_t e;
-    if (l == 0) {
-      {
-        ProfScope ps(a.prof, CASR_K_DEC_LSTM, s);
-        DecLstmA asrc{a.W + a.L.emb16, d.st[0], d.tok[0], d.src[0], d.err, R, a.V, 1};
-        DecLstmEpi epi{a.W + a.L.dec_b, d.st[0], st_new, asrc, d.newdone, a.W + a.L.w_hidden, d.qpart, R, 0, R};
-        epi.hw = 1;
-        launch_dec_lstm(R, a.W + a.L.dec_w16, asrc, epi, 1, s);
-      }
-      ProfScope ps(a.prof, CASR_K_ATTENTION, s);
-      e = launch_attention_step(a, st_new, d.qpart, al, d.newdone, 0, R, s);
-    } else {
-      ProfScope ps(a.prof, CASR_K_ATTENTION, s);
-      AttnCell cell{};
-      cell.st_old = d.st[l & 1];
-      cell.gates = a.fb.gates;
-      cell.emb_gates = a.fb.emb_gates;
-      cell.w_hidden = a.W + a.L.w_hidden;
-      cell.tok = d.tok[l & 1];
-      cell.err = d.err;
-      cell.sel = fuse ? 1 : 0;
-      cell.gs = GreedySel{d.part, nbp, l - 1, a.max_len, a.eos, finished, out_len, accum, tokens, d.newdone};
-      e = launch_attention_cell_step(a, st_new, cell, al, d.newdone, l, R, s);
-    }
+    const GreedySel gs{d.part, nbp, l - 1, a.max_len, a.eos, finished, out_len, accum, tokens, d.newdone};
+    const hipError_t e = l == 0 ? decode_step(a, d, 0, R, al, s, nullptr, false)
+                                : fold_attention_step(a, d, l, R, al, fuse, gs, s);
     if (e != hipSuccess) return e;
     fold_gemm_step(a, d, l, R, s);
     if (fuse && l + 1 < a.max_len) continue;
@@ -1938,8 +1938,14 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
   hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, a.k,
                      a.sos, d.tok[0], d.src[0], d.score[0], nullptr);
   for (int l = 0; l < a.max_len; ++l) {
-    hipError_t e = decode_step(a, d, l, a.B, nullptr, s);
+    // the folded step (CASR_OPT_DEC_FOLD): step 0's LSTMCell + attention, then per step the
+    // attention with the cell prologue (l >= 1) and the fused GEMM
+    hipError_t e;
+    if (!a.fold) e = decode_step(a, d, l, a.B, nullptr, s);
+    else if (l == 0) e = decode_step(a, d, 0, a.B, nullptr, s, nullptr, false);
+    else e = fold_attention_step(a, d, l, a.B, nullptr, false, GreedySel{}, s);
     if (e != hipSuccess) return e;
+    if (a.fold) fold_gemm_step(a, d, l, a.B, s);
     ProfScope ps(a.prof, CASR_K_SELECT, s);
     if (a.k <= 2) launch_beam_select<4>(a, d, l, s);
     else if (a.k <= 4) launch_beam_select<8>(a, d, l, s);

@@ -539,6 +539,42 @@ def test_decode_fold_vs_three_launches(eng, name):
             np.testing.assert_allclose(f["alignment"].cpu().numpy(), u["alignment"].cpu().numpy(), atol=1e-5, rtol=0)
 
 
+@pytest.mark.parametrize("eos_bias", [0.0, None])
+@pytest.mark.parametrize("B", [128, 256])
+def test_beam_fold_vs_three_launches(eng, B, eos_bias):
+    """The folded beam step (CASR_OPT_DEC_FOLD at R >= 1024 rows: the fused projection | LSTM-gate
+    GEMM in its one-accumulator 128 x 224 / 256 x 224 shapes, logits, tile maxima and row partials
+    for the beam select; the cell at each row's predecessor inside the attention kernel) against the
+    three-launch step, beam 8 at B = 128 (R = 1024, BASELINE config 3) and B = 256 (R = 2048, the
+    metric's beam line), T = 800, with and without early finishers: identical tokens and lengths,
+    scores within 2e-3 (decoder.py:104-135, model.py:604-987)."""
+    kw = {} if eos_bias is None else {"eos_bias": eos_bias}
+    eng.bind(pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True, **kw)))
+    feat, flen = _bench_batch(eng, B)
+    eng.encode(feat, flen)
+    outs = []
+    for fold in (1, 0):
+        eng.set_option("DEC_FOLD", fold)
+        eng.profile(["dec_lstm"])
+        try:
+            r = {k: v.cpu() for k, v in eng.beam(8).items()}
+            n_lstm = eng.profile_read()["dec_lstm"][0]
+        finally:
+            eng.profile([])
+            eng.set_option("DEC_FOLD", 1)
+        assert eng.device_flags() == 0
+        outs.append((r, n_lstm))
+    (f, n_f), (u, n_u) = outs
+    assert n_u == CFG.max_len
+    assert n_f == (1 if eng.requested == "s16x3" else CFG.max_len)
+    assert torch.equal(f["length"], u["length"])
+    assert torch.equal(f["steps"], u["steps"])
+    for b in range(B):
+        n = int(u["length"][b])
+        assert torch.equal(f["tokens"][b, :n], u["tokens"][b, :n]), b
+    np.testing.assert_allclose(f["score"].numpy(), u["score"].numpy(), atol=2e-3, rtol=0)
+
+
 def test_bind_refuses_foreign_blob(eng):
     """A blob of another layout (size or stamp) is refused on bind, not read past its end."""
     from casr import lib as L
