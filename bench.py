@@ -45,8 +45,12 @@ def fbank_batch(first, B, T, F=80):
                      for b in range(B)])
 
 
-def kernel_work(cls, B, Tp, R, V, T):
-    """Algorithmic work of ONE step's launches of a kernel class: (flops or bytes, bound)."""
+def kernel_work(cls, B, Tp, R, V, T, fold=False):
+    """Algorithmic work of ONE step's launches of a kernel class: (flops or bytes, bound).
+    fold: the folded decode step (CASR_OPT_DEC_FOLD): the LSTMCell GEMM runs at
+    decode step 0 only, the projection class is the fused [W_p ; W_ch] GEMM (the next step's gate
+    columns at steps 0..38), the attention class also gathers the gates and the token's gate-table
+    row and writes h / c (its q product is on-chip)."""
     H, C, HD, E, A, D = 256, 512, 512, 256, 128, 720
     if cls == "input_proj":
         return 2.0 * B * Tp * 8 * H * (D + 3 * C), "mfma"
@@ -55,11 +59,12 @@ def kernel_work(cls, B, Tp, R, V, T):
     if cls == "keys":
         return 2.0 * B * Tp * A * C, "mfma"
     if cls == "dec_lstm":
-        return 40 * 2.0 * R * 4 * HD * (E + C + HD), "mfma"
+        return (1 if fold else 40) * 2.0 * R * 4 * HD * (E + C + HD), "mfma"
     if cls == "proj":
-        return 40 * 2.0 * R * V * (C + HD), "mfma"
+        return (40 * 2.0 * R * V + (39 * 2.0 * R * 4 * HD if fold else 0)) * (C + HD), "mfma"
     if cls == "attention":   # keys + values streamed once per utterance per step
-        return 40 * 4.0 * B * Tp * (A + C), "hbm"
+        cell = 39 * 4.0 * R * (2 * 4 * HD + HD + 3 * HD) if fold else 0.0
+        return 40 * 4.0 * B * Tp * (A + C) + cell, "hbm"
     if cls == "select":      # the greedy select reads ProjA's per-block (max, sum, argmax) partials,
         return 40 * 4.0 * 3 * R * 64, "hbm"  # never the [R, V] logits (fused select: one launch)
     if cls == "features":    # fbank read + the layer-0 s16 row image written (Kp = 768: 4 B per column)
@@ -80,12 +85,18 @@ LAUNCH_UNIT = {
 }
 
 
-def kernel_bytes(cls, B, Tp, R, V):
+def kernel_bytes(cls, B, Tp, R, V, fold=False):
     """Algorithmic HBM bytes of ONE launch of a kernel class (compulsory reads + writes), to set
     beside the PMC-measured traffic; None where not tabulated.  Weights are the s16 images (4 B
-    per element, like f32)."""
+    per element, like f32).  fold: as kernel_work."""
     H, C, D, A, E, HD = 256, 512, 720, 128, 256, 512
     VP = (V + 63) // 64 * 64
+    if fold and cls == "attention":  # + gates and gate-table rows gathered, c read, h / c / h16 written
+        return 4.0 * (B * Tp * (A + C) + R * (2 * 4 * HD + HD + 3 * HD))
+    if fold and cls == "proj":       # fused image (vocabulary + gate tiles), [ctx | h] rows, gates written
+        vt = (V + 15) // 16
+        return 4.0 * ((vt * 16 + 4 * HD) * (C + HD) + R * (C + HD) + R * 4 * HD + 3 * R * 64 +
+                      (R * V + R * vt if R > B else 0))
     if cls == "input_proj":  # average layer: X read, W_ih read, Gin written
         k = (D + 3 * C) / 4.0
         return 4.0 * (B * Tp * k + 8 * H * k + B * Tp * 8 * H)
@@ -307,10 +318,10 @@ def main():
     # committed PMC passes (tools/probes/profile_r03.sh): greedy step, and beam 8 at B = 256
     pmc_greedy, pmc_beam = load_pmc("pmc_traffic.json"), load_pmc("pmc_traffic_beam.json")
 
-    def roof(cls, launches, ms, steps, Bc, Rc, pmc=pmc_greedy):
+    def roof(cls, launches, ms, steps, Bc, Rc, pmc=pmc_greedy, fold=False):
         """Achieved rate of one kernel class: algorithmic work of `steps` steps over its launches'
         summed duration, against the peak of its bound; PMC columns from the committed passes."""
-        work, bound = kernel_work(cls, Bc, Tp, Rc, cfg.vocab, T)
+        work, bound = kernel_work(cls, Bc, Tp, Rc, cfg.vocab, T, fold)
         if not work or not launches or ms <= 0:
             return None
         per_launch = work * steps / launches
@@ -325,16 +336,20 @@ def main():
         rec_p = pmc.get(cls) or {}
         if rec_p.get("hbm_bytes"):
             out["traffic"] = float(rec_p["hbm_bytes"])
-            alg = kernel_bytes(cls, Bc, Tp, Rc, cfg.vocab)
+            alg = kernel_bytes(cls, Bc, Tp, Rc, cfg.vocab, fold)
             if alg:
                 out["traffic_over_algorithmic"] = out["traffic"] / alg
         if rec_p.get("mfma_busy") is not None:
             out["mfma_busy"] = rec_p["mfma_busy"]
         return out
 
-    dom = roof(dominant, dom_launches, dom_ms, args.steps, B, B)
+    # the folded decode step ran when the instrumented step launched the LSTMCell GEMM once
+    def folded(bd):
+        return bd.get("dec_lstm", (0, 0.0))[0] == 1
+    fold = folded(breakdown)
+    dom = roof(dominant, dom_launches, dom_ms, args.steps, B, B, fold=fold)
     # every class of the instrumented step (one step: launches and ms of that step)
-    kernels = {c: roof(c, n, ms, 1, B, B) for c, (n, ms) in breakdown.items()}
+    kernels = {c: roof(c, n, ms, 1, B, B, fold=fold) for c, (n, ms) in breakdown.items()}
     achieved, peak, unit, bound = dom["achieved"], dom["peak"], dom["unit"], dom["bound"]
     avg_launch_s = dom["avg_launch_us"] / 1e6
     traffic = dom.get("traffic")
@@ -360,7 +375,8 @@ def main():
                 "unit": "utt/s", "ms_per_step": 1000.0 * dtb / steps,
                 "rtf": dtb / steps / (Bb * world * AUDIO_S_PER_UTT),
                 "kernel_breakdown_ms": {c: round(v[1], 3) for c, v in bd.items()},
-                "kernels": {c: roof(c, n, ms, 1, Bb, Bb * k, pmc_beam if Bb == 256 and k == 8 else {})
+                "decode_step": "folded (2 launches + select)" if folded(bd) else "3 launches + select",
+                "kernels": {c: roof(c, n, ms, 1, Bb, Bb * k, pmc_beam if Bb == 256 and k == 8 else {}, folded(bd))
                             for c, (n, ms) in bd.items()}}
 
     beam = config3 = None
@@ -519,6 +535,8 @@ def main():
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
             "rtf": dt / args.steps / (B * world * AUDIO_S_PER_UTT),
             "decode_launch": "hipGraph replay" if args.graphs else "eager launches",
+            "decode_step": "folded (2 launches per step: attention with the LSTM cell, fused projection | "
+                           "gate GEMM)" if fold else "3 launches per step (LSTMCell, attention, projection)",
             "beam": beam,
             "config3_beam8_b128": config3,
             "roofline": {"kernel": dominant, "bound": bound, "achieved": achieved, "peak": peak,

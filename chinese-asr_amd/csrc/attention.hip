@@ -132,18 +132,34 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   const int len = min(lens[b], Tp);
   const size_t row0 = (size_t)b * k + j0;
 
+  // score work split (phase 2): G a-groups of apg keys rows x Tq / 4 chunks of 4 steps
+  const int nch = Tq / 4;
+  const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
+  const int apg = (A + G - 1) / G;
+  const float* kb = keysT + (size_t)b * A * Tq;
+  const float* ekb = ekT + (size_t)b * A * Tq;
+  constexpr int CH = KPB >= 8 ? AT_CH / 2 : AT_CH;  // KPB 8: half the keys rows per batch (registers)
+  // CELL: the first keys batch of this thread's first score item (split form) is loaded before the
+  // cell phase, which it does not depend on, so the scores start on landed keys
+  constexpr bool PRE = CELL == 1 || (CELL == 2 && KPB >= 8);  // (KPB 4: 20 keys rows per batch, no registers left)
+  float4 kvp[PRE ? CH : 1];
+  if constexpr (PRE) {
+    const int ag = tid / nch, t0 = 4 * (tid - ag * nch), a0 = ag * apg, a1 = min(A, a0 + apg);
+    const bool live = !direct && tid < G * nch && t0 < len;
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      kvp[i] = live && a0 + i < a1 ? *reinterpret_cast<const float4*>(ekb + (size_t)(a0 + i) * Tq + t0)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if constexpr (CELL == 1) {
     // 0. the folded step's LSTM cell (decoder.py:104-114) and query (attention.py:92) for row r.
-    // W_hidden slice (rows 32 us .. +31, columns 4 a4 .. +3), the previous step's gate
-    // pre-activations of unit u = tid and its c are loaded first: none depends on the select
+    // The previous step's gate pre-activations of unit u = tid and its c are loaded first (with the
+    // keys above and the select's partials: none depends on the select); the W_hidden slice (rows
+    // 32 us .. +31, columns 4 a4 .. +3) with the token's gate-table row, after the select
     __shared__ int tk_s, skip_s;
     const int r = (int)row0;
     const int a4 = tid & (A / 4 - 1), us = tid / (A / 4);
     constexpr int UPS = HD / AT_QS;  // units per query slice
-    float4 wh[UPS];
-#pragma unroll
-    for (int i = 0; i < UPS; ++i)
-      wh[i] = *reinterpret_cast<const float4*>(cell.w_hidden + (size_t)(UPS * us + i) * A + 4 * a4);
     const int u = tid;
     auto gcol = [](int g, int u) { return (u >> 4) * 64 + g * 16 + (u & 15); };  // packed_gate_row
     float gprev[4];
@@ -206,6 +222,10 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float eg[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) eg[g] = cell.emb_gates[(size_t)t * (4 * HD) + gcol(g, u)];
+    float4 wh[UPS];
+#pragma unroll
+    for (int i = 0; i < UPS; ++i)
+      wh[i] = *reinterpret_cast<const float4*>(cell.w_hidden + (size_t)(UPS * us + i) * A + 4 * a4);
     float h2, c2;
     lstm_cell_hw(gprev[0] + eg[0], gprev[1] + eg[1], gprev[2] + eg[2], gprev[3] + eg[3], cold, h2, c2);
     st[(size_t)r * ST + C + u] = h2;
@@ -234,14 +254,14 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   }
   if constexpr (CELL == 2) {
     // 0. the folded beam step's LSTM cell for the block's nk rows r = row0 + j: token tok[r],
-    // predecessor s = src[r] (clamped and reported like DecLstmA::bind).  Thread = unit u; h rows
-    // [KPB][HD] and the query slices [AT_THREADS / A][KPB][A] in the score scratch (free until the
-    // scores).  q: thread (column a, slice us of 128 units), an f32 fma chain per row in unit
-    // order, the slices added in slice order.
-    float* hsb = xs;
-    float* qsl = xs + KPB * HD;
-    constexpr int NS = AT_THREADS / A, UPS = HD / NS;
-    const int a = tid & (A - 1), us = tid / A;
+    // predecessor s = src[r] (clamped and reported like DecLstmA::bind); thread = unit u.  Then
+    // q = h . W_hidden for the block's rows as s16x3 MFMAs (the split words of h, rows padded to 16,
+    // in the score scratch, free until the scores; W_hidden^T's fragment image wq16): wave w owns
+    // attention columns 16 w .. 16 w + 15 over all HD units (16 k-steps of 32), so no partial sums
+    // cross waves.  Its fragments are loaded before the cells, under the gathers.
+    constexpr int HS16 = HD + 4;  // row stride in words: 16 B skew per row, conflict-free b128 reads
+    static_assert(KPB * HS16 <= attn_scratch_floats<KPB>(4), "h rows fit the scratch");
+    uint32_t* hs16 = reinterpret_cast<uint32_t*>(xs);
     const int u = tid;
     auto gcol = [](int g, int u) { return (u >> 4) * 64 + g * 16 + (u & 15); };  // packed_gate_row
     int sr[KPB], tk[KPB], bad = 0;
@@ -265,9 +285,17 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       }
       co[j] = cell.st_old[(size_t)sr[j] * ST + C + HD + u];
     }
-    float whs[UPS];  // W_hidden[UPS us + i][a], in flight under the cells
+    constexpr int QKS = HD / 32;  // k-steps of the query MFMAs
+    f16x8 bh[QKS], bl[QKS];
+    {
+      const float* wb = cell.wq16 + (size_t)wv * (HD / 64) * FRAG;
 #pragma unroll
-    for (int i = 0; i < UPS; ++i) whs[i] = cell.w_hidden[(size_t)(UPS * us + i) * A + a];
+      for (int ks = 0; ks < QKS; ++ks) {
+        const float* fb = wb + (size_t)(ks >> 1) * FRAG + (ks & 1) * 512 + ln * 4;
+        bh[ks] = *reinterpret_cast<const f16x8*>(fb);
+        bl[ks] = *reinterpret_cast<const f16x8*>(fb + 256);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < KPB; ++j) {
       float h2 = 0.f, c2;
@@ -279,26 +307,30 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
         st[r * ST + C + HD + u] = c2;
         reinterpret_cast<uint32_t*>(st)[r * ST + ST16 + C + u] = split16_word(h2);
       }
-      hsb[j * HD + u] = h2;
+      hs16[j * HS16 + u] = j < nk ? split16_word(h2) : 0u;
     }
     __syncthreads();
-    float qa[KPB];
+    f32x4 qh = {0.f, 0.f, 0.f, 0.f}, qx = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < KPB; ++j) qa[j] = 0.f;
+    for (int ks = 0; ks < QKS; ++ks) {
+      // lane (row ln & 15, g = ln >> 4) of k-step ks: units 64 (ks >> 1) + 16 g + 8 (ks & 1) + e
+      // (MFMA rows KPB..15 are zero operands)
+      const int hr = ln & 15;
+      const uint32_t* hp = hs16 + min(hr, KPB - 1) * HS16 + 64 * (ks >> 1) + 16 * (ln >> 4) + 8 * (ks & 1);
+      u32x4 w0 = *reinterpret_cast<const u32x4*>(hp), w1 = *reinterpret_cast<const u32x4*>(hp + 4);
+      if (hr >= KPB) w0 = w1 = u32x4{0u, 0u, 0u, 0u};
+      f16x8 ah, al;
+      unpack16(w0, w1, ah, al);
+      mfma_s16(ah, al, bh[ks], bl[ks], qh, qx);
+    }
 #pragma unroll
-    for (int i = 0; i < UPS; ++i)
-#pragma unroll
-      for (int j = 0; j < KPB; ++j) qa[j] = fmaf(hsb[j * HD + UPS * us + i], whs[i], qa[j]);
-#pragma unroll
-    for (int j = 0; j < KPB; ++j) qsl[(us * KPB + j) * A + a] = qa[j];
-    __syncthreads();
-    for (int f = tid; f < KPB * A; f += AT_THREADS) {
-      const int j = f / A, c = f - j * A;
-      float q = qsl[j * A + c];
-#pragma unroll
-      for (int i = 1; i < NS; ++i) q += qsl[(i * KPB + j) * A + c];
-      qs[c * KPB + j] = j < nk ? q : 0.f;
-      eqs[c * KPB + j] = j < nk ? split_exp2x(q) : 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const int j = 4 * (ln >> 4) + i, c = 16 * wv + (ln & 15);
+      if (j < KPB) {
+        const float q = s16_combine(qh[i], qx[i]);
+        qs[c * KPB + j] = j < nk ? q : 0.f;
+        eqs[c * KPB + j] = j < nk ? split_exp2x(q) : 0.f;
+      }
     }
     __syncthreads();  // the score phase overwrites the scratch
   }
@@ -337,10 +369,6 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     eqs[(4 * a4 + 3) * KPB + j] = j < nk ? split_exp2x(q.w) : 0.f;
   }
   for (int i = tid; i < KPB * (AT_APAD - A); i += AT_THREADS) qs[A * KPB + i] = eqs[A * KPB + i] = 0.f;
-  // score work split: G a-groups of apg keys rows x Tq / 4 chunks of 4 steps
-  const int nch = Tq / 4;
-  const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
-  const int apg = (A + G - 1) / G;
   if (tid < A) {
     const float v = vv[tid];
     vs[tid] = v;
@@ -353,9 +381,6 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   // all loaded before use; partial sums per a-group go to LDS and are added in group order.
   // Split form (ekT, see split_exp2x) unless `direct` or a NaN score sends the block back to the
   // direct tanh(k + q) over keysT.
-  const float* kb = keysT + (size_t)b * A * Tq;
-  const float* ekb = ekT + (size_t)b * A * Tq;
-  constexpr int CH = KPB >= 8 ? AT_CH / 2 : AT_CH;  // KPB 8: half the keys rows per batch (registers)
   // this thread's score work: (a-group, 4-step chunk) items it = tid, tid + 512, ...; each in
   // batches of CH keys rows
   bool nan_seen = false;  // a NaN score of this thread's items (split form: leave it to the direct form)
@@ -421,7 +446,12 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     int ab = a0;
     if (first) {  // straight-line first batch: no loop join between its wait and its use
       float4 kv[CH];
-      load(kv, ab);
+      if constexpr (PRE && split) {  // preloaded before the cell phase (it == tid)
+#pragma unroll
+        for (int i = 0; i < CH; ++i) kv[i] = kvp[i];
+      } else {
+        load(kv, ab);
+      }
       after_loads();
       if (live) batch(kv, ab);
       ab += CH;

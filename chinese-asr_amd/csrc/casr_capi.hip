@@ -177,7 +177,7 @@ struct casr_handle {
   DevBuf x16;                       // s16 row image of the current layer input [B*Tp][Kp]
   // folded greedy decode (CASR_OPT_DEC_FOLD): fused projection | LSTM-gate fragment image and the
   // per-token gate table, built at bind from an s16-valid blob; the gates buffer [R][4 HD]
-  DevBuf wfold, egates, fgates;
+  DevBuf wfold, egates, fgates, wq16;
   bool fold_ready = false;
   bool s16() const { return precision == CASR_PREC_S16X3 && s16_valid; }
   int B = 0, Tp = 0;
@@ -464,7 +464,8 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
     const int V = h->cfg.vocab;
     HIP_OK(h, h->wfold.ensure((size_t)(fold_vtiles(V) + FOLD_GT) * (KPROJ / 64) * FRAG * sizeof(float)));
     HIP_OK(h, h->egates.ensure((size_t)V * 4 * HD * sizeof(float)));
-    HIP_OK(h, build_fold(h->W, h->L, V, h->wfold.as<float>(), h->egates.as<float>(), nullptr));
+    HIP_OK(h, h->wq16.ensure(FOLD_WQ16_FLOATS * sizeof(float)));
+    HIP_OK(h, build_fold(h->W, h->L, V, h->wfold.as<float>(), h->egates.as<float>(), h->wq16.as<float>(), nullptr));
     HIP_OK(h, hipStreamSynchronize(nullptr));
     h->fold_ready = true;
   }
@@ -496,7 +497,7 @@ void casr_destroy(casr_handle* h) {
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->gflags, &h->fe_const,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout, &h->wfold,
-                    &h->egates, &h->fgates})
+                    &h->egates, &h->fgates, &h->wq16})
     b->release();
   delete h;
 }
@@ -910,7 +911,7 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   a.fold = (k == 1 || fold_beam) && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
   if (a.fold) {
     HIP_OK(h, h->fgates.ensure((size_t)R * 4 * HD * sizeof(float)));
-    a.fb = FoldBufs{h->wfold.as<float>(), h->egates.as<float>(), h->fgates.as<float>()};
+    a.fb = FoldBufs{h->wfold.as<float>(), h->egates.as<float>(), h->wq16.as<float>(), h->fgates.as<float>()};
   }
   return CASR_OK;
 }

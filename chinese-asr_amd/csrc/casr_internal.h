@@ -310,13 +310,16 @@ __device__ __forceinline__ void greedy_book(const GreedySel& gs, int r, int t, f
 constexpr int FOLD_GT = 4 * HD / 16;  // LSTM gate tiles (16 gate rows each) in the fused image
 constexpr int FOLD_NT = 7;            // 16-column tiles per fused GEMM block (112 columns)
 inline int fold_vtiles(int V) { return (V + 15) / 16; }
+constexpr size_t FOLD_WQ16_FLOATS = (size_t)A * HD;  // the W_hidden fragment image (beam query)
 struct FoldBufs {
   const float* wfold;      // s16 fragment image: [fold_vtiles(V) + FOLD_GT tiles][KPROJ / 64] FRAG blocks
   const float* emb_gates;  // [V][4 HD] packed gate-row order (packed_gate_row), biases included
+  const float* wq16;       // s16 fragment image of W_hidden^T: [A / 16 tiles][HD / 64] FRAG blocks
   float* gates;            // [R][4 HD] the next step's [ctx | h] . W_ch^T, packed gate-row order
 };
 // build the fused image and the per-token gate table from a bound s16-valid blob (bind time)
-hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, hipStream_t s);
+hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, float* wq16,
+                      hipStream_t s);
 
 struct DecodeBufs {
   float* st[2];          // [R][ST]
@@ -377,6 +380,7 @@ struct AttnCell {
   const float* gates;
   const float* emb_gates;
   const float* w_hidden;  // [HD][A]
+  const float* wq16;      // beam: FoldBufs::wq16
   const int32_t* tok;     // sel == 0 (beam: the select's tokens of the block's rows)
   const int32_t* src;     // beam: the predecessor row of each row (gates_prev and c are read there)
   int32_t* err;

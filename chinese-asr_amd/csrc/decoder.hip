@@ -652,7 +652,7 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
 template <int NTN>
 __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const float (&bn)[16], int row0, int nb,
                                                 int u, float* scr, float* logits, float* tmx, int R, int V,
-                                                int ntl) {
+                                                int ntl, float* gates = nullptr, int gcol0 = 0) {
   constexpr int RWS = 16 * NTN + 4, CH = 4 * NTN;  // slab row stride; float4 per tile row
   const int lane = threadIdx.x & 63, g = lane >> 4;
 #pragma unroll
@@ -668,6 +668,11 @@ __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const f
     const int f = i * 64 + lane, rr = f / CH, ch = f - rr * CH;
     const float4 v = *reinterpret_cast<const float4*>(scr + rr * RWS + 4 * ch);
     const int row = rb0 + rr, col = c0 + 4 * ch;
+    if (gates && col >= gcol0) {  // (FoldEpi) the next step's gate pre-activations: raw, no bias
+      if (row < R && col - gcol0 < 4 * HD) *reinterpret_cast<float4*>(gates + (size_t)row * (4 * HD) + (col - gcol0)) = v;
+      continue;
+    }
+    if (!logits) continue;
     if (row < R) {
       float* dst = logits + (size_t)row * V + col;
       if (vec && col + 3 < V) {
@@ -801,18 +806,14 @@ struct FoldEpi {
   template <int NTN>
   __device__ __forceinline__ void run(const f32x4 (&acc)[NTN], int row0, int nb, int u, const Pre& p,
                                       float* scr) const {
-#pragma unroll
-    for (int tn = 0; tn < NTN; ++tn) {
-      const int gt = nb * NTN + tn - VT;
-      if (gt < 0 || gt >= FOLD_GT) continue;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = row0 + e;
-        if (row < R) gates[(size_t)row * (4 * HD) + gt * 16 + u] = acc[tn][e];
-      }
-    }
+    // logits (beam) and the gate columns through the wave's LDS slab as float4 row segments (the
+    // gate columns of consecutive tiles are consecutive in gates[row]; VT 16 is a multiple of 4, so
+    // no segment straddles the two); the biases of the gate tiles are 0 (Pre), the stored values raw
+    const bool has_gates = (nb + 1) * NTN > VT;
+    if (logits || has_gates)
+      proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, VT, has_gates ? gates : nullptr,
+                           16 * VT);
     if (nb * NTN >= VT) return;  // no vocabulary tile in this block
-    if (logits) proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, VT);
     if (gp.mx) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
   }
 };
@@ -862,13 +863,30 @@ __global__ __launch_bounds__(256) void fold_emb_gates_kernel(const float* __rest
     if (v0 + j < V) out[(size_t)(v0 + j) * (4 * HD) + n] = acc[j] + b;
 }
 
-hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, hipStream_t s) {
+// W_hidden^T ([A][HD]: n = attention column, k = decoder unit) as an s16 fragment image (the layout
+// of casr_capi.hip pack_frag16: block (nt, kc) = [j][hi | lo][lane][8 halves], n = 16 nt + (lane & 15),
+// k = 64 kc + 16 (lane >> 4) + 8 j + e): the B operand of the beam cell's query MFMAs
+__global__ void fold_wq16_kernel(const float* __restrict__ w_hidden, float* __restrict__ out) {
+  const int blk = blockIdx.x, nt = blk / (HD / 64), kc = blk % (HD / 64);
+  uint16_t* o = reinterpret_cast<uint16_t*>(out) + (size_t)blk * FRAG * 2;
+  for (int i = threadIdx.x; i < 2 * 64 * 8; i += blockDim.x) {  // (j, lane, e)
+    const int j = i / 512, lane = (i / 8) % 64, e = i % 8;
+    const int n = nt * 16 + (lane & 15), k = kc * 64 + 16 * (lane >> 4) + 8 * j + e;
+    const uint32_t w = split16_word(w_hidden[(size_t)k * A + n]);
+    o[((j * 2 + 0) * 64 + lane) * 8 + e] = (uint16_t)(w & 0xFFFFu);
+    o[((j * 2 + 1) * 64 + lane) * 8 + e] = (uint16_t)(w >> 16);
+  }
+}
+
+hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, float* wq16,
+                      hipStream_t s) {
   const int VT = fold_vtiles(V);
   if (VT > L.VP / 16) return hipErrorInvalidValue;
   hipLaunchKernelGGL(fold_image_kernel, dim3((VT + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w16,
                      W + L.dec_w16, VT, wfold);
   hipLaunchKernelGGL(fold_emb_gates_kernel, dim3((V + FOLD_EV - 1) / FOLD_EV, 4 * HD / 256), dim3(256), 0, s,
                      W + L.emb, W + L.dec_w, W + L.dec_b, V, emb_gates);
+  hipLaunchKernelGGL(fold_wq16_kernel, dim3((A / 16) * (HD / 64)), dim3(256), 0, s, W + L.w_hidden, wq16);
   return hipGetLastError();
 }
 
@@ -1712,7 +1730,8 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
 // the folded step's GEMM (KB) over the 441 tiles (313 vocabulary + 128 gate) of the fused image.
 // Greedy: 64 x 112 blocks (R <= 32: 32 x 112), ring of three 64-deep stages (44 KB each); at R = 256,
 // 4 x 63 = 252 blocks in one round, 721 KB per block against 590 KB (projection) + 491 KB
-// (LSTMCell) for the three-launch step.  Beam (one-accumulator s16x3, 32-deep stages, wave tiles of
+// (LSTMCell) for the three-launch step (a ring of six 32-deep stages, the same bits, measured
+// 1.29-1.34 against 1.00 ms per greedy batch).  Beam (one-accumulator s16x3, 32-deep stages, wave tiles of
 // 16 RS rows x 112 columns, the 7-tile column blocks of the greedy shapes): 256 x 224 blocks, ring
 // of two 60 KB stages, at R >= 2048 (8 x 32 = 256 blocks at R = 2048, 1.97 MB each against 1.7 MB
 // + 1.3 MB); 128 x 224, ring of three, below (R = 1024: 256 blocks)
@@ -1724,7 +1743,7 @@ static void launch_fold_gemm(int R, bool beam, int NB, int ntiles, const float* 
   if (!beam) {
     if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
     else launch_dg<4, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
-  } else if (dec_wide(R)) {
+  } else if (dec_wide(R)) {  // (128 x 224 in two rounds at R = 2048 measured 12.07 against 11.47 ms per batch)
     launch_dg<4, FOLD_NT_BEAM, 2, 4, 2, true, 32, true>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
   } else {
     launch_dg<4, FOLD_NT_BEAM, 3, 2, 2, true, 32, true>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
@@ -1842,6 +1861,7 @@ static hipError_t fold_attention_step(const DecodeArgs& a, DecodeBufs& d, int l,
   cell.gates = a.fb.gates;
   cell.emb_gates = a.fb.emb_gates;
   cell.w_hidden = a.W + a.L.w_hidden;
+  cell.wq16 = a.fb.wq16;
   cell.tok = d.tok[l & 1];
   cell.src = d.src[l & 1];
   cell.err = d.err;
