@@ -18,19 +18,29 @@ from collections import defaultdict
 
 # bench.py kernel classes -> (kernel-name prefixes after short(), launches of the class per step
 # as bench.py counts them: one "launch" of input_proj = one layer's projection, persistent kernel
-# and half-tile tail together)
+# and half-tile tail together; None = one launch per dispatch, counted: the folded decode step
+#  launches the LSTMCell GEMM once per decode and its fused GEMM is the proj class)
 CLASS_OF = {
     "input_proj": (("gemm16_persist_kernel", "gemm16_bias_kernel"), 4),
     "rec_step": (("rec_layer_kernel",), 4),
     "keys": (("gemm_nt_kernel<KeysEpi",), 1),
-    "dec_lstm": (("dgemm_kernel<2, 4, 4, DecLstmA", "dgemm_kernel<4, 4, 4, DecLstmA", "dgemm_kernel<8, 8, 4, DecLstmA",
-                  "dgemm_kernel<8, 8, 2, DecLstmA"), 40),
-    "proj": (("dgemm_kernel<2, 5, 4, ProjA", "dgemm_kernel<4, 5, 4, ProjA", "dgemm_kernel<8, 5, 3, ProjA",
-              "dgemm_kernel<4, 10, 2, ProjA", "dgemm_kernel<8, 10, 3, ProjA"), 40),
-    "select": (("beam_select_kernel",), 40),
-    "attention": (("attention_kernel",), 40),
+    "dec_lstm": (("dgemm_kernel<*DecLstmA",), None),
+    "proj": (("dgemm_kernel<*ProjA",), None),
+    "select": (("beam_select_kernel",), None),
+    "attention": (("attention_kernel",), None),
     "features": (("features_stats_kernel", "features_rows_kernel"), 1),
 }
+
+
+def matches(name, pres):
+    for p in pres:
+        if "*" in p:
+            a, b = p.split("*")
+            if name.startswith(a) and b in name:
+                return True
+        elif name.startswith(p):
+            return True
+    return False
 
 
 def short(name):
@@ -78,13 +88,16 @@ def main(d, json_out=None):
     steps = int(os.environ.get("STEPS", 2))
     for cls, (pres, per_step) in CLASS_OF.items():
         tot = defaultdict(float)
+        ndisp = 0
         for (name, grid), cs in per.items():
-            if any(name.startswith(p) for p in pres):
+            if matches(name, pres):
                 for c, v in cs.items():
                     tot[c] += sum(v)
+                ndisp += len(cs.get("FETCH_SIZE", []))
         if "FETCH_SIZE" not in tot:
             continue
-        launches = steps * per_step
+        launches = steps * per_step if per_step else ndisp
+        per_step = per_step or ndisp / steps
         fetch = 2 * tot["FETCH_SIZE"] * 1024 / launches  # KB -> B, gfx950 x2
         write = tot.get("WRITE_SIZE", 0.0) * 1024 / launches
         rec = {"fetch_bytes": fetch, "write_bytes": write, "hbm_bytes": fetch + write,
