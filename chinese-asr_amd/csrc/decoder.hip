@@ -120,8 +120,13 @@ __device__ __forceinline__ void static_for(F&& f) {
 // sum scaled by 2^11, acc += a_hi (w_hi 2^11) + a_hi w_lo' + a_lo' w_hi (w_hi 2^11 formed by one
 // v_pk_mul_f16, exact while |w| < 32), as the encoder's input projection (gemm16.hip): half the
 // accumulator registers of the (hi.hi, cross) pair, which the 256 x 160 block cannot hold.
+// SA > S (the 256-row beam blocks; S = 2): the A tiles get a deeper ring of their own (SA stage
+// buffers of A, S of W) and each step issues the next W stage BEFORE the A stage SA - 1 ahead, so the
+// counted wait for stage kt retires only W(kt) (and what preceded it) while A(kt + SA - 2) stays in
+// flight: the chain waits on a 28 KB W stage instead of a 60 KB [A | W] one.  Same operands, same
+// order per element: bitwise equal to SA = S.
 template <int WR, int NT, int S, class ASrc, class Epi, bool S16 = false, int RS = 1, int WC = 1, bool IL = false,
-          int BKW = 64, bool ONE = false>
+          int BKW = 64, bool ONE = false, int SA = S>
 __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntiles, int nkt,
                                                     const float* __restrict__ Wf, ASrc asrc, Epi epi) {
   constexpr int KQ = 8 / (WR * WC), QPW = 4 / KQ, BM = 16 * WR * RS, NTW = NT / WC;
@@ -137,14 +142,26 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   constexpr int NSLOT = (NDMA + 7) / 8;      // per wave (at most)
   const int nkb = B32 ? nkt / 2 : nkt;        // 64-deep fragment blocks per W column tile
   static_assert(S >= 2 && S <= 6, "ring of 2..6 stage buffers");
-  static_assert(S * STG * 4 <= 160 * 1024, "ring fits the LDS");
+  static_assert((S * STG + (SA - S) * ATILE) * 4 <= 160 * 1024, "ring fits the LDS");
   static_assert((S - 2) * NSLOT < 64, "vmcnt range");
+  constexpr bool ASYM = SA > S;
+  constexpr int JA = NA / 8;  // ASYM: slots j < JA are A DMAs in every wave, the rest W
+  static_assert(!ASYM || (S == 2 && SA <= 4 && NA % 8 == 0 && JA < NSLOT), "deeper A ring: S = 2, whole A slots");
   __shared__ __attribute__((aligned(16))) float lb0[STG];
   __shared__ __attribute__((aligned(16))) float lb1[STG];
   __shared__ __attribute__((aligned(16))) float lb2[S > 2 ? STG : 4];
   __shared__ __attribute__((aligned(16))) float lb3[S > 3 ? STG : 4];
   __shared__ __attribute__((aligned(16))) float lb4[S > 4 ? STG : 4];
   __shared__ __attribute__((aligned(16))) float lb5[S > 5 ? STG : 4];
+  __shared__ __attribute__((aligned(16))) float lx0[SA > S ? ATILE : 4];  // ASYM: A stage buffers S, S + 1
+  __shared__ __attribute__((aligned(16))) float lx1[SA > S + 1 ? ATILE : 4];
+  // ASYM: A slot a of the A ring (A part of lb0 / lb1, then lx0, lx1); W slot of the W ring: lb0 / lb1
+  auto abuf = [&](auto I) -> float* {
+    if constexpr (I == 0) return lb0;
+    else if constexpr (I == 1) return lb1;
+    else if constexpr (I == 2) return lx0;
+    else return lx1;
+  };
   auto buf = [&](auto I) -> float* {
     if constexpr (I == 0) return lb0;
     else if constexpr (I == 1) return lb1;
@@ -171,21 +188,36 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   int bad = 0;
   // (a source with one segment (kSeg == 0) keeps one pointer per slot; W sources are 32-bit
   // offsets from Wf: registers the 256 x 160 block needs for its accumulators)
+  // (one-segment sources: 32-bit offsets from the source's row 0 as well)
   constexpr int NSEG = ASrc::kSeg > 0 ? 2 : 1;
-  const float* aseg[NSLOT][NSEG];
+  constexpr bool AOFF = NSEG == 1;
+  const float* aseg[AOFF ? 1 : NSLOT][NSEG];
+  uint32_t aoff[AOFF ? NSLOT : 1];
+  const float* abase = nullptr;
+  if constexpr (AOFF) {
+    const float* s1;
+    int unused = 0;
+    asrc.bind(0, abase, s1, unused);
+  }
   uint32_t woff[NSLOT];
 #pragma unroll
   for (int j = 0; j < NSLOT; ++j) {
     const int i = w + 8 * j;
     woff[j] = 0;
+    if constexpr (AOFF) aoff[j] = 0;
+    else
 #pragma unroll
-    for (int q = 0; q < NSEG; ++q) aseg[j][q] = nullptr;
+      for (int q = 0; q < NSEG; ++q) aseg[j][q] = nullptr;
     if (i < NA) {
       const float* s0;
       const float* s1;
       asrc.bind(rb * BM + RPI * i + lane / (64 / RPI), s0, s1, bad);
-      aseg[j][0] = s0;
-      aseg[j][NSEG - 1] = s1;
+      if constexpr (AOFF) {
+        aoff[j] = (uint32_t)(s0 - abase);
+      } else {
+        aseg[j][0] = s0;
+        aseg[j][NSEG - 1] = s1;
+      }
     } else if (i < NDMA) {
       const int tn = (i - NA) / WPI, qq = (i - NA) % WPI;
       int t = nb * NT + tn;
@@ -193,15 +225,16 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       woff[j] = (uint32_t)(t * nkb * FRAG + qq * 256 + lane * 4);
     }
   }
-  auto stage_slot = [&](float* dst, int kt, auto J) {
+  // dst: the stage's [A | W] buffer, or (ASYM) da / dw: its A and W buffers
+  auto stage_slot2 = [&](float* la, float* lw, int kt, auto J) {
     constexpr int j = decltype(J)::value;
     if constexpr (j < NSLOT) {
-      float* la = dst;
-      float* lw = dst + ATILE;
       const int kb = B32 ? kt >> 1 : kt, k0 = kb * 64;
       const int i = w + 8 * j;
       if (i < NA) {
-        const float* seg = k0 < ASrc::kSeg ? aseg[j][0] + k0 : aseg[j][NSEG - 1] + (k0 - ASrc::kSeg);
+        const float* seg;
+        if constexpr (AOFF) seg = abase + aoff[j] + k0;
+        else seg = k0 < ASrc::kSeg ? aseg[j][0] + k0 : aseg[j][NSEG - 1] + (k0 - ASrc::kSeg);
         if constexpr (B32) {
           const int row = 8 * i + (lane >> 3), p = (lane & 7) ^ (row & 7);
           lds_dma16(seg + 16 * (p >> 1) + 8 * (kt & 1) + 4 * (p & 1), la + i * 256);
@@ -215,6 +248,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       }
     }
   };
+  auto stage_slot = [&](float* dst, int kt, auto J) { stage_slot2(dst, dst + ATILE, kt, J); };
   auto stage = [&](float* dst, int kt) { static_for<0, NSLOT>([&](auto J) { stage_slot(dst, kt, J); }); };
   constexpr bool ILS = IL && S16;
 
@@ -227,9 +261,8 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       if constexpr (!ONE) accx[rs][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   auto arow = [&](int rs) { return (ws * RS + rs) * 16 + r; };
-  auto compute = [&](const float* src, int kt, auto&& issue) {
-    const float* la = src;
-    const float* lw = src + ATILE + wc * NTW * WFR;
+  auto compute2 = [&](const float* la, const float* lw0, int kt, auto&& issue) {
+    const float* lw = lw0 + wc * NTW * WFR;
     if constexpr (S16) {
       bool pend = ILS;  // DMA slots of the next tile not issued yet (wave-uniform)
 #pragma unroll
@@ -304,10 +337,20 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
         }
     }
   };
+  auto compute = [&](const float* src, int kt, auto&& issue) { compute2(src, src + ATILE, kt, issue); };
 
-  static_for<0, S - 1>([&](auto I) {
-    if (I < nkt) stage(buf(I), I);
-  });
+  if constexpr (ASYM) {
+    // issue order A(0), W(0), A(1) .. A(SA - 2): each later step issues W(kt + 1), then A(kt + SA - 1)
+    static_for<0, JA>([&](auto J) { stage_slot2(abuf(std::integral_constant<int, 0>{}), lb0, 0, J); });
+    static_for<JA, NSLOT>([&](auto J) { stage_slot2(lb0, lb0 + ATILE, 0, J); });
+    static_for<1, SA - 1>([&](auto I) {
+      if (I < nkt) static_for<0, JA>([&](auto J) { stage_slot2(abuf(I), lb0, I, J); });
+    });
+  } else {
+    static_for<0, S - 1>([&](auto I) {
+      if (I < nkt) stage(buf(I), I);
+    });
+  }
   // after the first ring stages are in flight: the epilogue's operands (bias, predecessor rows,
   // W_hidden), loaded under the k loop, and the early-exit check (its wait also retires those
   // stages: a skipped block leaves no DMA behind)
@@ -323,7 +366,40 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   if (epi.skip()) return;
   if (bad) atomicOr(epi.err_flags(), bad);
   stamp(1);
-  for (int kt0 = 0; kt0 < nkt; kt0 += S) {
+  if constexpr (ASYM) {
+    // unrolled by the W ring's period; the A buffer is picked at run time (wave-uniform): the DMAs are
+    // inline asm, so hipcc adds no wait for them whatever it can prove about the buffers
+    auto abuf_rt = [&](int a) -> float* { return a == 0 ? lb0 : a == 1 ? lb1 : a == 2 ? lx0 : lx1; };
+    for (int kt0 = 0; kt0 < nkt; kt0 += 2) {
+      static_for<0, 2>([&](auto I) {
+        const int kt = kt0 + I;
+        if (kt >= nkt) return;
+        // W(kt) was issued at step kt - 1, followed only by that step's A(kt + SA - 2)
+        vm_wait_le<JA>(kt + SA - 2 < nkt ? JA : 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // issue position p: W slots first (p < NSLOT - JA), then A
+        auto issue = [&](auto P) {
+          constexpr int p = decltype(P)::value, j = (p + JA) % NSLOT;
+          if constexpr (j >= JA) {
+            if (kt + 1 < nkt && !(CASR_DG_DIAG & 1))
+              stage_slot2(lb0, buf(std::integral_constant<int, (I + 1) % 2>{}) + ATILE, kt + 1,
+                          std::integral_constant<int, j>{});
+          } else {
+            if (kt + SA - 1 < nkt && !(CASR_DG_DIAG & 1))
+              stage_slot2(abuf_rt((kt + SA - 1) % SA), lb0, kt + SA - 1, std::integral_constant<int, j>{});
+          }
+        };
+        if constexpr (!ILS) static_for<0, NSLOT>(issue);
+        if (kt == 0) stamp(2);
+        if (!(CASR_DG_DIAG & 2))
+          compute2(abuf_rt(kt % SA), buf(std::integral_constant<int, I % 2>{}) + ATILE, kt, issue);
+        else if constexpr (ILS) static_for<0, NSLOT>(issue);
+      });
+    }
+  }
+  for (int kt0 = 0; !ASYM && kt0 < nkt; kt0 += S) {
     static_for<0, S>([&](auto I) {
       const int kt = kt0 + I;
       if (kt >= nkt) return;
@@ -399,14 +475,14 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   stamp(4);
 }
 
-template <int WR, int NT, int S, int RS = 1, int WC = 1, bool IL = false, int BKW = 64, bool ONE = false, class ASrc,
-          class Epi>
+template <int WR, int NT, int S, int RS = 1, int WC = 1, bool IL = false, int BKW = 64, bool ONE = false, int SA = S,
+          class ASrc, class Epi>
 static void launch_dg(int NB, int R, int ntiles, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi,
                       int s16, hipStream_t s) {
   constexpr int BM = 16 * WR * RS;
   const int NR = (R + BM - 1) / BM;
   if constexpr (BKW == 32 || ONE) {  // s16 only (the f32 form of the same shape does not fit the LDS)
-    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL, BKW, ONE>), dim3(xcd_grid(NB, NR)),
+    hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL, BKW, ONE, SA>), dim3(xcd_grid(NB, NR)),
                        dim3(512), 0, s, NB, NR, ntiles, nkt * (64 / BKW), Wf, asrc, epi);
   } else {
     if (s16)
@@ -1732,8 +1808,8 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
 // 4 x 63 = 252 blocks in one round, 721 KB per block against 590 KB (projection) + 491 KB
 // (LSTMCell) for the three-launch step (a ring of six 32-deep stages, the same bits, measured
 // 1.29-1.34 against 1.00 ms per greedy batch).  Beam (one-accumulator s16x3, 32-deep stages, wave tiles of
-// 16 RS rows x 112 columns, the 7-tile column blocks of the greedy shapes): 256 x 224 blocks, ring
-// of two 60 KB stages, at R >= 2048 (8 x 32 = 256 blocks at R = 2048, 1.97 MB each against 1.7 MB
+// 16 RS rows x 112 columns, the 7-tile column blocks of the greedy shapes): 256 x 224 blocks, a W ring
+// of two 28 KB stages and an A ring of three 32 KB stages (dgemm_kernel SA), at R >= 2048 (8 x 32 = 256 blocks at R = 2048, 1.97 MB each against 1.7 MB
 // + 1.3 MB); 128 x 224, ring of three, below (R = 1024: 256 blocks)
 constexpr int FOLD_NT_BEAM = 2 * FOLD_NT;
 template <class ASrc, class Epi>
@@ -1744,7 +1820,9 @@ static void launch_fold_gemm(int R, bool beam, int NB, int ntiles, const float* 
     if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
     else launch_dg<4, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
   } else if (dec_wide(R)) {  // (128 x 224 in two rounds at R = 2048 measured 12.07 against 11.47 ms per batch)
-    launch_dg<4, FOLD_NT_BEAM, 2, 4, 2, true, 32, true>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+    // A ring of three beside the W ring of two (152 KB): fused GEMM 3.96-4.02 -> 3.88-3.92 ms per beam
+    // batch (interleaved A/B, two rounds; a version unrolled by 6 with static A buffers spilled 11 VGPRs)
+    launch_dg<4, FOLD_NT_BEAM, 2, 4, 2, true, 32, true, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
   } else {
     launch_dg<4, FOLD_NT_BEAM, 3, 2, 2, true, 32, true>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
   }
