@@ -27,6 +27,7 @@ constexpr int GB_M = 128, GB_N = 128, GB_K = 32;
 
 struct StoreBiasEpi {  // C[row][col] = acc + bias[col]; N % 4 == 0, rows 16 B aligned
   static constexpr bool kRowTile = true;
+  static constexpr bool kColTile = false;
   float* C;
   const float* bias;
   int ldc;
@@ -39,8 +40,15 @@ struct StoreBiasEpi {  // C[row][col] = acc + bias[col]; N % 4 == 0, rows 16 B a
 // keysT[b][a][t] = acc + b_attn[a], row = b*Tp + t, row stride Tq; and behind the B x A x Tq keys,
 // ekT = exp(2 keys) for the attention's split exponential score form (attention.hip split_exp2x:
 // v_exp_f32 of keys * 2 log2(e), NaN where |keys| >= 43, which sends a block to the direct form)
+// The tile (128 rows m = b Tp + t x 128 columns a) goes out transposed (kColTile): staged through LDS
+// as [a][m] in two 64-column passes, then written as float4 runs along t of keysT[b][a][.] (each
+// (b, a) row is contiguous in t; Tq is a multiple of 4, so a quad t = 4q .. 4q + 3 is 16-B aligned;
+// quads that cross the tile's first or last row or an utterance boundary are stored per element,
+// each element by the tile that owns its row).  The scalar per-element form wrote 4-B pieces 1 KB
+// apart (PMC: 129 MB written for 70 MB of keys and e^{2 keys}).
 struct KeysEpi {
   static constexpr bool kRowTile = false;
+  static constexpr bool kColTile = true;
   float* keysT;
   const float* bias;
   int Tp, Tq, B;
@@ -255,6 +263,61 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float* __restrict
         }
       }
       __syncthreads();
+    }
+  } else if constexpr (Epi::kColTile) {
+    // [a][m] staging, 64 columns per pass (the waves with wn == pass), rows XOR-swizzled by the
+    // column (phys row = m ^ 4 (a & 15)): the 16 columns of a store hit 16 bank groups; a 4-aligned
+    // run of rows stays contiguous
+    static_assert(GB_N == 128 && GB_M == 128 && 64 * GB_M <= 2 * TILE, "a 64-column pass fits one stage buffer");
+    const int Mt = min(GB_M, M - m0);  // rows of this tile
+    const int b0 = m0 / epi.Tp, b1 = (m0 + Mt - 1) / epi.Tp;  // the utterances the tile spans
+    const size_t eoff = (size_t)epi.B * A * epi.Tq;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      __syncthreads();  // the ring (or the previous pass) is no longer read
+      if (wn == pass) {
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int a = tn * 16 + r, m = wm * 64 + tm * 16 + g * 4 + e;  // a within the pass
+              buf0[a * GB_M + (m ^ ((a & 15) << 2))] = acc[tm][tn][e];
+            }
+      }
+      __syncthreads();
+      // per utterance segment b: t in [ta, tb], quads qa .. qa + nq - 1, thread = (column, quad)
+      for (int b = b0; b <= b1; ++b) {
+        const int ta = max(0, m0 - b * epi.Tp), tb = min(epi.Tp - 1, m0 + Mt - 1 - b * epi.Tp);
+        const int qa = ta >> 2, nq = (tb >> 2) - qa + 1;
+        for (int it = tid; it < 64 * nq; it += 256) {
+          const int a = it & 63, t4 = (qa + (it >> 6)) * 4;
+          const int col = n0 + pass * 64 + a;
+          const float bv = epi.bias[col];
+          float v[4];
+          bool ok[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int t = t4 + j, m = b * epi.Tp + t - m0;  // row within the tile
+            ok[j] = t >= ta && t <= tb;
+            v[j] = ok[j] ? buf0[a * GB_M + (m ^ ((a & 15) << 2))] + bv : 0.f;
+          }
+          float* kp = epi.keysT + ((size_t)b * A + col) * epi.Tq + t4;
+          if (ok[0] && ok[1] && ok[2] && ok[3]) {
+            *reinterpret_cast<float4*>(kp) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<float4*>(kp + eoff) =
+                make_float4(split_exp2x(v[0]), split_exp2x(v[1]), split_exp2x(v[2]), split_exp2x(v[3]));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (ok[j]) {
+                kp[j] = v[j];
+                kp[eoff + j] = split_exp2x(v[j]);
+              }
+          }
+        }
+      }
     }
   } else {
 #pragma unroll
