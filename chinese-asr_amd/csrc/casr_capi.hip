@@ -908,7 +908,9 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   // one-accumulator beam shapes, decoder.hip launch_fold_gemm)
   const bool fold_beam = k > 1 && R >= 1024 && h->proj_small && h->dec_small &&
                          attention_kpb(B, k, h->tune[CASR_OPT_ATTN_KPB]) >= 4;
-  a.fold = (k == 1 || fold_beam) && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
+  // (a vocabulary beyond the 64 seven-tile partial blocks of the fused GEMM keeps the three-launch step)
+  const bool fold_vocab = (fold_vtiles(V) + FOLD_NT - 1) / FOLD_NT <= GP_NB;
+  a.fold = (k == 1 || fold_beam) && fold_vocab && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
   if (a.fold) {
     HIP_OK(h, h->fgates.ensure((size_t)R * 4 * HD * sizeof(float)));
     a.fb = FoldBufs{h->wfold.as<float>(), h->egates.as<float>(), h->wq16.as<float>(), h->fgates.as<float>()};
