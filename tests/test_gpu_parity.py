@@ -575,6 +575,29 @@ def test_beam_fold_vs_three_launches(eng, B, eos_bias):
     np.testing.assert_allclose(f["score"].numpy(), u["score"].numpy(), atol=2e-3, rtol=0)
 
 
+def test_fold_graph_replay_equals_eager(eng):
+    """The folded decode step captured and replayed as a hipGraph (casr_set_graphs mode 1) equals
+    its eager launches bit for bit: greedy at B = 128 and beam 8 at B = 128 (R = 1024 rows, the
+    folded beam shape), the second replay from the cached graph."""
+    eng.bind(pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True)))
+    feat, flen = _bench_batch(eng, 128)
+    eng.encode(feat, flen)
+    outs = []
+    try:
+        for graphs in (False, True, True):
+            eng.set_graphs(3 if graphs else 0)
+            g = eng.greedy()
+            bm = eng.beam(8)
+            assert eng.device_flags() == 0
+            outs.append([x.cpu() for x in (g["tokens"], g["accum"], g["out_len"], bm["tokens"], bm["score"],
+                                           bm["length"], bm["steps"])])
+    finally:
+        eng.set_graphs(2)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a, b)
+
+
 def test_bind_refuses_foreign_blob(eng):
     """A blob of another layout (size or stamp) is refused on bind, not read past its end."""
     from casr import lib as L
