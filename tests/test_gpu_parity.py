@@ -540,14 +540,15 @@ def test_decode_fold_vs_three_launches(eng, name):
 
 
 @pytest.mark.parametrize("eos_bias", [0.0, None])
-@pytest.mark.parametrize("B", [128, 256])
-def test_beam_fold_vs_three_launches(eng, B, eos_bias):
+@pytest.mark.parametrize("B,k", [(128, 8), (256, 8), (128, 16)])
+def test_beam_fold_vs_three_launches(eng, B, k, eos_bias):
     """The folded beam step (CASR_OPT_DEC_FOLD at R >= 1024 rows: the fused projection | LSTM-gate
     GEMM in its one-accumulator 128 x 224 / 256 x 224 shapes, logits, tile maxima and row partials
     for the beam select; the cell at each row's predecessor inside the attention kernel) against the
-    three-launch step, beam 8 at B = 128 (R = 1024, BASELINE config 3) and B = 256 (R = 2048, the
-    metric's beam line), T = 800, with and without early finishers: identical tokens and lengths,
-    scores within 2e-3 (decoder.py:104-135, model.py:604-987)."""
+    three-launch step: beam 8 at B = 128 (R = 1024, BASELINE config 3) and B = 256 (R = 2048, the
+    metric's beam line), beam 16 at B = 128 (R = 2048 with 4 of an utterance's 16 rows per attention
+    block, BASELINE config 5's shape); T = 800, with and without early finishers: identical tokens
+    and lengths, scores within 2e-3 (decoder.py:104-135, model.py:604-987)."""
     kw = {} if eos_bias is None else {"eos_bias": eos_bias}
     eng.bind(pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True, **kw)))
     feat, flen = _bench_batch(eng, B)
@@ -557,7 +558,7 @@ def test_beam_fold_vs_three_launches(eng, B, eos_bias):
         eng.set_option("DEC_FOLD", fold)
         eng.profile(["dec_lstm"])
         try:
-            r = {k: v.cpu() for k, v in eng.beam(8).items()}
+            r = {n: v.cpu() for n, v in eng.beam(k).items()}
             n_lstm = eng.profile_read()["dec_lstm"][0]
         finally:
             eng.profile([])
