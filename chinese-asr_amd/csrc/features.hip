@@ -139,7 +139,10 @@ __global__ __launch_bounds__(256) void cmvn_kernel(float* __restrict__ feat,
 // [0, nf) (stack_kernel's); mean = the 24 chunk sums (each in row order) added in a fixed tree,
 // / lp; var likewise over (v - mean)^2 / (lp - 1); std = sqrt(var) + eps (main.py:37).
 constexpr int SM = 8, SRM = 3 * SM, SPH = 24, SQ = 9 * SM;  // mels, (frame, mel) pairs, chunks, dims
-constexpr int FS_MAX_T = 1024;  // stats kernel's LDS: nf x SM floats (32 KB) + 7 KB
+constexpr int FS_MAX_T = 1024;  // stats kernel's LDS: (nf + 14) x SM floats (33 KB) + 7 KB
+// zero frames staged before / after the nf frames: windows reach t = -4 and, with the refill after
+// a chunk's last row, t = 3 lp + 6 <= nf + 6; FS_PAD2 = 10 covers it (the refill's values are unused)
+constexpr int FS_PAD = 4, FS_PAD2 = 10;
 constexpr int RJ = 16, RNF = 3 * RJ + 8, RTH = 384;
 static_assert(F % SM == 0 && 2 * RTH >= D, "mel slabs tile the 80 mels; a block's pairs cover a row");
 
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(SRM * SPH) void features_stats_kernel(const float* 
                                                                    const int32_t* __restrict__ frames, int B, int T,
                                                                    float eps, float* __restrict__ stats,
                                                                    int32_t* __restrict__ feat_len) {
-  extern __shared__ float xs[];  // [nf][SM]
+  extern __shared__ float xs[];  // [FS_PAD + nf + FS_PAD2][SM]: frames -4 .. nf + 9, zero outside [0, nf)
   __shared__ float part[SPH][SQ];
   __shared__ float mean_s[SQ];
   // 1-D grid, XCD-aware: the F / SM slab blocks of one utterance take ids with equal id % 8, so
@@ -176,14 +179,20 @@ __global__ __launch_bounds__(SRM * SPH) void features_stats_kernel(const float* 
 #pragma unroll
   for (int u = 0; u < NLD; ++u) {
     const int i = tid + u * SRM * SPH;
-    if (i < nf * (SM / 4)) *reinterpret_cast<float4*>(xs + (i / (SM / 4)) * SM + 4 * (i % (SM / 4))) = ld[u];
+    if (i < nf * (SM / 4)) *reinterpret_cast<float4*>(xs + (FS_PAD + i / (SM / 4)) * SM + 4 * (i % (SM / 4))) = ld[u];
+  }
+  // the zero frames either side, so the windows below read LDS with no bounds test (a test per
+  // read made every window load a branch: half the kernel's instructions were exec-mask handling)
+  if (tid < (FS_PAD + FS_PAD2) * (SM / 4)) {
+    const int fz = tid / (SM / 4), f = fz < FS_PAD ? fz : nf + fz;
+    *reinterpret_cast<float4*>(xs + f * SM + 4 * (tid % (SM / 4))) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
   // pair rm = r * SM + mm; its dims q = c * SRM + rm  ->  output column c*240 + r*80 + m0 + mm
   const int r = rm / SM, mm = rm % SM;
   const DeltaTaps taps = make_taps();
   const int ch = (lp + SPH - 1) / SPH, ja = min(ph * ch, lp), jb = min(ja + ch, lp);
-  auto frame = [&](int t) { return (t >= 0 && t < nf) ? xs[t * SM + mm] : 0.f; };
+  auto frame = [&](int t) { return xs[(t + FS_PAD) * SM + mm]; };  // t in [-4, nf + 9]
   auto sweep = [&](auto&& use) {
     float win[9];  // frames t-4 .. t+4 of t = 3 j + r
 #pragma unroll
@@ -342,7 +351,7 @@ hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int
   if (Tp <= 0 || B <= 0) return hipErrorInvalidValue;
   // eps < 0: no CMVN (the stacked features get_log_mel returns, data.py:226-249)
   if (T <= FS_MAX_T) {
-    const size_t shm = (size_t)T * SM * sizeof(float);
+    const size_t shm = (size_t)(T + FS_PAD + FS_PAD2) * SM * sizeof(float);
     hipLaunchKernelGGL(features_stats_kernel, dim3((F / SM) * ((B + 7) / 8 * 8)), dim3(SRM * SPH), shm, s, fbank, frames, B, T, eps, stats,
                        feat_len);
     hipLaunchKernelGGL(features_rows_kernel<false>, dim3((Tp + RJ - 1) / RJ, B), dim3(RTH), 0, s, fbank, frames, T, Tp,
@@ -363,7 +372,7 @@ hipError_t launch_features_x16(const float* fbank, const int32_t* frames, int B,
                                int32_t* feat_len, float* stats, uint16_t* x16, int Kp, int32_t* err, hipStream_t s) {
   const int Tp = T / 3;
   if (B <= 0 || !features_x16_supported(T) || Kp != 2 * RTH) return hipErrorInvalidValue;
-  const size_t shm = (size_t)T * SM * sizeof(float);
+  const size_t shm = (size_t)(T + FS_PAD + FS_PAD2) * SM * sizeof(float);
   hipLaunchKernelGGL(features_stats_kernel, dim3((F / SM) * ((B + 7) / 8 * 8)), dim3(SRM * SPH), shm, s, fbank, frames, B, T, eps, stats,
                      feat_len);
   hipLaunchKernelGGL(features_rows_kernel<true>, dim3((Tp + RJ - 1) / RJ, B), dim3(RTH), 0, s, fbank, frames, T, Tp,
