@@ -85,7 +85,7 @@ LAUNCH_UNIT = {
 }
 
 
-def kernel_bytes(cls, B, Tp, R, V, fold=False):
+def kernel_bytes(cls, B, Tp, R, V, fold=False, s16=True):
     """Algorithmic HBM bytes of ONE launch of a kernel class (compulsory reads + writes), to set
     beside the PMC-measured traffic; None where not tabulated.  Weights are the s16 images (4 B
     per element, like f32).  fold: as kernel_work."""
@@ -100,8 +100,10 @@ def kernel_bytes(cls, B, Tp, R, V, fold=False):
     if cls == "input_proj":  # average layer: X read, W_ih read, Gin written
         k = (D + 3 * C) / 4.0
         return 4.0 * (B * Tp * k + 8 * H * k + B * Tp * 8 * H)
-    if cls == "rec_step":    # Gin read, layer output written (h exchange is on-chip traffic)
-        return 4.0 * (B * Tp * 8 * H + B * Tp * C)
+    if cls == "rec_step":    # average layer: Gin read, layer output written, the residual input read
+        # (layers 1-3), and the next layer's s16 row image written by the cells (the last layer's
+        # feeds the keys GEMM; s16x3 only); the h exchange is on-chip traffic
+        return 4.0 * B * Tp * (8 * H + C + 0.75 * C + (C if s16 else 0))
     if cls == "attention":
         return 4.0 * B * Tp * (A + C)
     if cls == "dec_lstm":    # W image, the gathered A rows, new h / c / h16 and the query partials
@@ -278,19 +280,32 @@ def main():
 
     flags = {}  # device guard bits read after every timed region (read and clear: all its steps)
 
+    step_ms = {}  # per-step device time (HIP events on the compute stream around each step)
+
     def timed(fn, steps, tag, e=None):
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
+        evs[0].record()
+        for i in range(steps):
             fn()
+            evs[i + 1].record()
         torch.cuda.synchronize()
         barrier()
         dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         if dist is not None:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
         flags[tag] = (e or eng).device_flags()
+        step_ms[tag] = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
         return float(dt.item())
+
+    def step_stats(tag):
+        v = sorted(step_ms.get(tag, []))
+        if not v:
+            return None
+        return {"median": v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2]),
+                "min": v[0], "max": v[-1], "n": len(v)}
 
     CLASSES = ["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"]
     for _ in range(args.warmup):
@@ -336,7 +351,7 @@ def main():
         rec_p = pmc.get(cls) or {}
         if rec_p.get("hbm_bytes"):
             out["traffic"] = float(rec_p["hbm_bytes"])
-            alg = kernel_bytes(cls, Bc, Tp, Rc, cfg.vocab, fold)
+            alg = kernel_bytes(cls, Bc, Tp, Rc, cfg.vocab, fold, precision == "s16x3")
             if alg:
                 out["traffic_over_algorithmic"] = out["traffic"] / alg
         if rec_p.get("mfma_busy") is not None:
@@ -372,6 +387,7 @@ def main():
         bd = eng.profile_read()
         eng.profile([])
         return {"k": k, "batch_per_gpu": Bb, "value": Bb * world * steps / dtb, "steps": steps,
+                "device_ms_per_step": step_stats(tag),
                 "unit": "utt/s", "ms_per_step": 1000.0 * dtb / steps,
                 "rtf": dtb / steps / (Bb * world * AUDIO_S_PER_UTT),
                 "kernel_breakdown_ms": {c: round(v[1], 3) for c, v in bd.items()},
@@ -402,6 +418,7 @@ def main():
         step_small()
         dts = timed(step_small, args.steps, "config2")
         small = {"config": "BASELINE config 2: greedy, B=32/GPU, T=800", "batch_per_gpu": Bs,
+                 "device_ms_per_step": step_stats("config2"),
                  "value": Bs * world * args.steps / dts, "unit": "utt/s", "ms_per_step": 1000.0 * dts / args.steps}
 
     # BASELINE config 1: one 8 s WAV, greedy, through the drop-in main.parse (main.py:27-65):
@@ -534,6 +551,9 @@ def main():
                                    f"encoder + 40-step attention decode, ids to host",
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
             "rtf": dt / args.steps / (B * world * AUDIO_S_PER_UTT),
+            "device_ms_per_step": step_stats("greedy"),
+            "device_ms_note": "per timed step, HIP events on the compute stream around each step (device "
+                              "time incl. any launch gaps; SURVEY 8d: median of the steps)",
             "decode_launch": "hipGraph replay" if args.graphs else "eager launches",
             "decode_step": "folded (2 launches per step: attention with the LSTM cell, fused projection | "
                            "gate GEMM)" if fold else "3 launches per step (LSTMCell, attention, projection)",
@@ -542,7 +562,7 @@ def main():
             "roofline": {"kernel": dominant, "bound": bound, "achieved": achieved, "peak": peak,
                          "unit": unit, "frac": achieved / peak, "traffic": traffic,
                          "traffic_unit": "bytes per launch (PMC 2 x FETCH_SIZE + WRITE_SIZE)",
-                         "algorithmic_bytes": kernel_bytes(dominant, B, Tp, B, cfg.vocab),
+                         "algorithmic_bytes": kernel_bytes(dominant, B, Tp, B, cfg.vocab, fold, precision == "s16x3"),
                          "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s,
                          "launch": LAUNCH_UNIT.get(dominant, "one kernel launch"),
                          "peak_basis": ("f16 MFMA dense peak / 3 (s16x3 f32-equivalent)" if bound == "mfma" and
@@ -568,6 +588,7 @@ def main():
         if cpu:
             rec["speedup_vs_cpu"] = value / cpu["value"]
         print(json.dumps(rec), flush=True)
+    eng.close()  # drain and free the handle now, not from __del__ at interpreter exit
     if dist is not None:
         dist.destroy_process_group()
 

@@ -4,8 +4,10 @@ PyTorch supplies device memory, the current HIP stream and (for multi-GPU) RCCL;
 compute step is a call into the HIP C-ABI library.  There is no CPU or torch-op fallback:
 without a GPU or the library, construction raises.
 """
+import atexit
 import ctypes
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -26,6 +28,21 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+# Every live Engine, closed at interpreter exit before module teardown: a handle's device work is
+# drained and its buffers freed while the HIP runtime (and a profiler attached to it) is still
+# fully up, not from __del__ during finalisation in whatever order the garbage collector picks.
+_LIVE = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    for e in list(_LIVE):
+        try:
+            e.close()
+        except Exception:
+            pass
+
+
 class Engine:
     """casr handle bound to packed weights on one device."""
 
@@ -39,6 +56,7 @@ class Engine:
         self.handle = ctypes.c_void_p()
         c = _lib.config_struct(cfg)
         _lib.check(self.lib.casr_create(ctypes.byref(c), self.device.index, ctypes.byref(self.handle)))
+        _LIVE.add(self)
         self.packed = None
         if packed is None and enc_sd is not None:
             packed = _lib.pack_weights(cfg, enc_sd, dec_sd)
@@ -67,9 +85,11 @@ class Engine:
         _lib.check(self.lib.casr_bind_weights(self.handle, _ptr(self.packed)), self.handle)
 
     def close(self):
+        """Destroy the handle (casr_destroy drains the device first).  Idempotent."""
         if self.handle:
             self.lib.casr_destroy(self.handle)
             self.handle = ctypes.c_void_p()
+        _LIVE.discard(self)
 
     def __del__(self):
         try:
@@ -207,9 +227,10 @@ class Engine:
         self.requested = precision
 
     def check_flags(self):
-        """Guard bits of the last encode / decode (synchronises).  Raises CasrError when the
-        recurrence hand-off timed out (bit 32: the encode's results are invalid); returns the
-        bits otherwise, so a caller can re-run at f32 on bit 128 (FLAG_F16_RANGE)."""
+        """Guard bits raised since the previous read (read and clear, casr_device_flags: every
+        encode / decode since then is covered; synchronises).  Raises CasrError when a recurrence
+        hand-off timed out (bit 32: those encoder results are invalid); returns the bits
+        otherwise, so a caller can re-run at f32 on bit 128 (FLAG_F16_RANGE)."""
         f = self.device_flags()
         if f & FLAG_REC_TIMEOUT:
             raise _lib.CasrError("persistent recurrence hand-off wait expired (device flag 32): "
@@ -219,7 +240,9 @@ class Engine:
     def run_checked(self, encode, decode):
         """encode(); out = decode(); then the guard bits.  Bit 32 raises; bit 128 (an s16x3
         operand beyond the f16 range) re-runs encode + decode on the exact-f32 path, so no
-        result rests on a wrong split image."""
+        result rests on a wrong split image.  Bits left by earlier unchecked calls are read and
+        discarded first, so only this batch's bits decide."""
+        self.device_flags()
         encode()
         out = decode()
         f = self.check_flags()

@@ -29,11 +29,13 @@ EXPORTS = [
 PRECISIONS = {"f32": 0, "s16x3": 1}
 
 # tuning options (include/casr.h CASR_OPT_*): speed only, every value gives the same bits, except
-# ATTN_DIRECT (the direct tanh(k + q) attention scores) and DEC_FOLD (the two-launch greedy step:
-# the same arithmetic regrouped): numerics variants within tolerance, the same token ids
+# ATTN_DIRECT (the direct tanh(k + q) attention scores) and DEC_FOLD (the folded decode step: two
+# launches per step, greedy always, beam at R >= 1024 rows with the one-accumulator fused GEMM; the
+# same arithmetic regrouped): numerics variants within tolerance, the same token ids.
+# REC_COOP_REFUSE is for tests: layer n - 1's cooperative launch is treated as refused
 OPTIONS = {"FUSE_SELECT": 0, "REC_LAYOUT": 1, "REC_STORE_PLAIN": 2, "REC_SLEEP": 3, "REC_POLL_GAP": 4,
            "REC_COOP": 5, "GEMM16_PERSIST": 6, "GEMM16_TAIL": 7, "ATTN_KPB": 8, "ATTN_DIRECT": 9,
-           "DEC_FOLD": 10}
+           "DEC_FOLD": 10, "REC_COOP_REFUSE": 11}
 
 # kernel classes of casr_profile_enable / casr_profile_read (include/casr.h)
 KERNEL_CLASSES = ["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"]

@@ -754,10 +754,10 @@ hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qp
   }
 }
 
-size_t attention_smem_bytes(int B, int k, int Tp, int opt) {
+size_t attention_smem_bytes(int B, int k, int Tp, int opt, int cell) {
   size_t f;
   switch (attention_kpb(B, k, opt)) {
-    case 1: f = attn_smem_floats<1>(Tp); break;
+    case 1: f = cell == 1 ? attn_smem_floats<1, 1>(Tp) : attn_smem_floats<1>(Tp); break;
     case 2: f = attn_smem_floats<2>(Tp); break;
     case 8: f = attn_smem_floats<8>(Tp); break;
     default: f = attn_smem_floats<4>(Tp); break;

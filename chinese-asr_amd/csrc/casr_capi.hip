@@ -488,6 +488,10 @@ int casr_get_precision(const casr_handle* h) {
 void casr_destroy(casr_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
+  // work enqueued on any stream may still read the handle's buffers (a persistent recurrence
+  // layer, a decode loop on the caller's stream, a graph replay on the private streams): drain
+  // the device before graphs, streams and buffers go away
+  (void)hipDeviceSynchronize();
   h->graphs.clear();
   if (h->cap) (void)hipStreamDestroy(h->cap);
   for (int i = 0; i < 2; ++i) {
@@ -531,8 +535,8 @@ int casr_recurrence_mode(const casr_handle* h, int B) {
 int casr_set_option(casr_handle* h, int option, int value) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
-  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0};
-  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8, 1, 1};
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8, 1, 1, CASR_MAX_LAYERS};
   if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
     return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
   if (value < lo[option] || value > hi[option])
@@ -689,7 +693,9 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
         HIP_OK(h, hipMemsetAsync(tbuf.p, 0, tbytes, s));
       }
       hipError_t er;
-      {
+      if (h->tune[CASR_OPT_REC_COOP_REFUSE] == l + 1) {
+        er = hipErrorCooperativeLaunchTooLarge;  // tests only: this layer's launch "refused"
+      } else {
         ProfScope ps(&h->prof, CASR_K_REC_STEP, s);
         // the last layer's image feeds the keys GEMM
         uint16_t* x16o = s16 ? h->x16.as<uint16_t>() : nullptr;
@@ -842,7 +848,7 @@ static bool decode_graph_ok(const casr_handle* h) {
   return (h->graph_mode & CASR_GRAPHS_DECODE) && !(h->prof.mask & dec);
 }
 
-static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
+static int prepare_decode(casr_handle* h, int k, DecodeArgs& a, bool greedy) {
   if (!h->encoded) return fail(h, CASR_ERR_STATE, "decode before casr_encode");
   if (k < 1 || k > KMAX_BEAM) return fail(h, CASR_ERR_ARG, "beam width %d not in [1, %d]", k, KMAX_BEAM);
   const int B = h->B, Tp = h->Tp, L = h->cfg.max_len, V = h->cfg.vocab;
@@ -903,14 +909,18 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a) {
   a.attn_kpb = h->tune[CASR_OPT_ATTN_KPB];
   a.attn_direct = h->tune[CASR_OPT_ATTN_DIRECT];
   a.proj_small = h->proj_small;
-  // the folded step: greedy (casr_greedy passes k = 1), or beam at R >= 1024 rows with 4 or 8 beam
-  // rows per attention block and every projection / LSTM weight < 16 (the fused GEMM's
-  // one-accumulator beam shapes, decoder.hip launch_fold_gemm)
-  const bool fold_beam = k > 1 && R >= 1024 && h->proj_small && h->dec_small &&
+  // the folded step: greedy (casr_greedy), or beam at R >= 1024 rows with 4 or 8 beam rows per
+  // attention block and every projection / LSTM weight < 16 (the fused GEMM's one-accumulator
+  // beam shapes, decoder.hip launch_fold_gemm).  casr_beam at k = 1 is a beam caller: it takes
+  // the beam guards, never the greedy clause (its fused GEMM would pick the one-accumulator shapes)
+  const bool fold_beam = !greedy && R >= 1024 && h->proj_small && h->dec_small &&
                          attention_kpb(B, k, h->tune[CASR_OPT_ATTN_KPB]) >= 4;
   // (a vocabulary beyond the 64 seven-tile partial blocks of the fused GEMM keeps the three-launch step)
   const bool fold_vocab = (fold_vtiles(V) + FOLD_NT - 1) / FOLD_NT <= GP_NB;
-  a.fold = (k == 1 || fold_beam) && fold_vocab && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
+  // the folded greedy attention (attention_kernel<1, 1>) holds its cell-phase area on top of the
+  // three-launch step's LDS: at Tp where only the latter fits, greedy keeps the three-launch step
+  const bool fold_lds = !greedy || attention_smem_bytes(B, k, Tp, h->tune[CASR_OPT_ATTN_KPB], 1) <= 160 * 1024;
+  a.fold = (greedy || fold_beam) && fold_vocab && fold_lds && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
   if (a.fold) {
     HIP_OK(h, h->fgates.ensure((size_t)R * 4 * HD * sizeof(float)));
     a.fb = FoldBufs{h->wfold.as<float>(), h->egates.as<float>(), h->wq16.as<float>(), h->fgates.as<float>()};
@@ -923,7 +933,7 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   if (!h || !tokens || !out_len || !finished || !accum) return fail(h, CASR_ERR_ARG, "casr_greedy: NULL output");
   HIP_OK(h, hipSetDevice(h->device));
   DecodeArgs a{};
-  int rc = prepare_decode(h, 1, a);
+  int rc = prepare_decode(h, 1, a, true);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   if (!decode_graph_ok(h)) {
@@ -965,7 +975,7 @@ int casr_beam(casr_handle* h, int k, float lm_weight, float length_weight, int32
     return fail(h, CASR_ERR_ARG, "casr_beam: NULL output");
   HIP_OK(h, hipSetDevice(h->device));
   DecodeArgs a{};
-  int rc = prepare_decode(h, k, a);
+  int rc = prepare_decode(h, k, a, false);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   h->dec_k = k;
@@ -1011,7 +1021,7 @@ int casr_beam_records(casr_handle* h, int32_t* rec_tokens, float* rec_score, uin
   if (!rec_tokens || !rec_score || !rec_valid) return fail(h, CASR_ERR_ARG, "casr_beam_records: NULL output");
   HIP_OK(h, hipSetDevice(h->device));
   DecodeArgs a{};
-  int rc = prepare_decode(h, h->dec_k, a);
+  int rc = prepare_decode(h, h->dec_k, a, false);
   if (rc) return rc;
   HIP_OK(h, run_beam_records(a, h->d, rec_tokens, rec_score, rec_valid, (hipStream_t)stream));
   return CASR_OK;

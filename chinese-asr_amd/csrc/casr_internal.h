@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0, 0, 1};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0, 0, 1, 0};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -190,12 +190,13 @@ struct CopyList {
 hipError_t copy_multi(const CopyList& cl, hipStream_t s);
 
 // frontend.hip: wav -> log-mel.  Constant tables live in one device struct per handle.
+constexpr int FE_FBW = 32;  // widest mel filter kept (nonzero bins; the widest has 17)
 struct FrontendConst {
-  float fb[257 * F];            // [bin][mel]
+  float fb[F][FE_FBW];          // filter m's nonzero weights, bins lo[m] .. hi[m] - 1
   int32_t lo[F], hi[F];         // nonzero bin range of each mel filter
   float win[400];               // periodic hann(400)
-  double tw256r[128], tw256i[128];  // exp(-2 pi i k / 256)
-  double tw512r[257], tw512i[257];  // exp(-2 pi i q / 512)
+  float tw256r[256], tw256i[256];  // exp(-2 pi i k / 256), rounded once from double
+  float tw512r[257], tw512i[257];  // exp(-2 pi i q / 512)
 };
 void mel_filterbank(int n_stft, float f_min, float f_max, int n_mels, float* fb);
 void build_frontend_const(FrontendConst* c);
@@ -389,7 +390,9 @@ struct AttnCell {
 };
 hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const AttnCell& cell, float* align,
                                       int32_t* newdone, int l, int total, hipStream_t s);
-size_t attention_smem_bytes(int B, int k, int Tp, int opt);
+// fixed LDS of the attention launch; cell = 1: the folded greedy step's attention_kernel<1, 1>
+// (its cell-phase area on top; CELL 2 keeps its cell data in the score scratch)
+size_t attention_smem_bytes(int B, int k, int Tp, int opt, int cell = 0);
 int attention_kpb(int B, int k, int opt);  // beam rows per attention block
 void attn_trace_bind(uint32_t* buf);  // CASR_DG_TRACE diagnostics (attention.hip)
 

@@ -1376,28 +1376,10 @@ __global__ __launch_bounds__(64 * bs_waves<K2>()) void beam_select_kernel(
       }
       nc = total;
     } else {
-    // this lane's largest and second-largest candidate values (for tau)
-    float lt, lt2 = -INFINITY;
-    // tau bound from the block partials only when they are at least twice as many as the 2k
-    // ranks (with as many blocks as ranks, e.g. k = 16 on 32 column blocks, the bound is the
-    // smallest block maximum: thousands of candidates pass it and the row falls back to the full
-    // selection); otherwise from the row's lane top-2s
-    const bool part_tau = UNIT_T && nbp >= 2 * n2k;
-    if (UNIT_T && nbp > 0) {
-      // from the projection's per-block partials (ProjEpi): lane c holds block c's max and
-      // sum exp(x - max); the block maxima are distinct elements, so their 2k-th largest
-      // bounds the row's 2k-th best value from below just as the lane maxima do
-      float mb = -INFINITY, sb = 0.f;
-      if (ln < nbp) {
-        mb = gp.mx[(size_t)(b * k + j) * GP_NB + ln];
-        sb = gp.se[(size_t)(b * k + j) * GP_NB + ln];
-      }
-      const float M = wave_max(mb);
-      const float s = wave_sum((sb > 0.f) ? sb * expf(mb - M) : 0.f);
-      lse = logf(s) + M;
-      lt = (mb - lse) + sc;
-    }
-    if (!part_tau) {
+    // the row read whole (temperature != 1, or a vocabulary beyond the tile-maxima table): the
+    // row's logsumexp and this lane's largest and second-largest candidate values (for tau)
+    float lt, lt2;
+    {
       float lm = -INFINITY, lm2 = -INFINITY;  // this lane's two largest x / T (distinct elements)
       auto top2 = [&](float y) {
         lm2 = fmaxf(lm2, fminf(lm, y));
@@ -1415,21 +1397,19 @@ __global__ __launch_bounds__(64 * bs_waves<K2>()) void beam_select_kernel(
       } else {
         for (int v = ln; v < V; v += 64) top2(xt(x[v]));
       }
-      if (!(UNIT_T && nbp > 0)) {
-        const float m = wave_max(lm);
-        float s = 0.f;
-        if (vec) {
+      const float m = wave_max(lm);
+      float s = 0.f;
+      if (vec) {
 #pragma unroll 4
-          for (int i = ln; i < V / 4; i += 64) {
-            const float4 q = x4[i];
-            s += expf(xt(q.x) - m) + expf(xt(q.y) - m) + expf(xt(q.z) - m) + expf(xt(q.w) - m);
-          }
-        } else {
-          for (int v = ln; v < V; v += 64) s += expf(xt(x[v]) - m);
+        for (int i = ln; i < V / 4; i += 64) {
+          const float4 q = x4[i];
+          s += expf(xt(q.x) - m) + expf(xt(q.y) - m) + expf(xt(q.z) - m) + expf(xt(q.w) - m);
         }
-        s = wave_sum(s);
-        lse = logf(s) + m;
+      } else {
+        for (int v = ln; v < V; v += 64) s += expf(xt(x[v]) - m);
       }
+      s = wave_sum(s);
+      lse = logf(s) + m;
       lt = (lm - lse) + sc;
       lt2 = (lm2 - lse) + sc;
     }

@@ -8,12 +8,16 @@
 //   mel    = P . fb  (fb [257][80], linspace(80, 7600, 257) bin-frequency quirk, data.py:43)
 //   out    = log(mel == 0 ? FLT_EPSILON : mel)               (data.py:223-224)
 //
-// One wave per frame, 4 frames in flight per 256-thread block.  The 512-point real transform is a
-// 256-point complex radix-2 FFT of z[m] = y[2m] + i y[2m+1] in LDS followed by the even/odd
-// split; it runs in fp64 so its rounding is far below the reference's own fp32 FFT error (the
-// oracle does the same, numpy float64 rfft).  Power and the mel projection are float32 like the
+// One wave per frame; a 256-thread block runs 4 waves, each over FE_FPW consecutive frames.  The
+// 512-point real transform is a 256-point complex FFT of z[m] = y[2m] + i y[2m+1] followed by the
+// even/odd split, all in float32 like the reference's torch.stft (data.py:205-221): four radix-4
+// decimation-in-frequency stages, each lane one butterfly of 4 points held in registers, the wave
+// exchanging points between stages through its own 2 KiB LDS buffer (no block barrier: a wave's LDS
+// operations complete in order).  The exchange address p ^ ((p >> 2) & 31) keeps every stage's
+// ds_write_b64 / ds_read_b64 free of bank conflicts.  A lane's window values and twiddles are the
+// same for every frame and stay in registers.  Power and the mel projection are float32 like the
 // reference.  Frames past an utterance's length are written as zeros.  The constant tables
-// (fb with per-filter nonzero ranges, window, twiddles) are built on the host in this file.
+// (per-filter nonzero weights, window, twiddles rounded once from double) are built on the host.
 #include <math.h>
 
 #include <vector>
@@ -26,7 +30,8 @@ namespace casr {
 namespace {
 constexpr int NFFT = 512, HOP = 160, WIN = 400, LPAD = (NFFT - WIN) / 2, NBIN = NFFT / 2 + 1;
 constexpr int NC = NFFT / 2;  // complex FFT size
-constexpr int FPB = 4;        // frames per block (one per wave)
+constexpr int FE_WAVES = 4;   // waves (frames in flight) per block
+constexpr int FE_FPW = 8;     // consecutive frames per wave
 
 // torch's elementwise steps, each rounded (no FMA contraction: hipcc's default would fuse them):
 // pre-emphasis x[t+1] - 0.97 x[t] (data.py:201-202), the window product, |X|^2 = re^2 + im^2
@@ -40,17 +45,48 @@ CASR_DEV float power2(float re, float im) {
   return re * re + im * im;
 }
 
-__device__ __forceinline__ int bitrev8(int x) { return (int)(__brev((unsigned)x) >> 24); }
+// exchange slot of FFT position p (conflict-free for the four stage patterns)
+CASR_DEV int fe_slot(int p) { return p ^ ((p >> 2) & 31); }
+// base-4 digit reversal of an 8-bit index: after the four DIF stages X[k] sits at position rev4(k)
+CASR_DEV int rev4(int k) {
+  return ((k & 3) << 6) | (((k >> 2) & 3) << 4) | (((k >> 4) & 3) << 2) | ((k >> 6) & 3);
+}
+CASR_DEV float2 cmul(float2 a, float2 w) { return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x); }
+
+// one radix-4 DIF butterfly: y_q = sum_r a_r (-i)^(rq), then y_q *= w_q (q = 1..3)
+CASR_DEV void bfly4(float2 (&a)[4], const float2 (&w)[3], bool twiddle) {
+  const float2 t0 = make_float2(a[0].x + a[2].x, a[0].y + a[2].y), t1 = make_float2(a[0].x - a[2].x, a[0].y - a[2].y);
+  const float2 t2 = make_float2(a[1].x + a[3].x, a[1].y + a[3].y), t3 = make_float2(a[1].x - a[3].x, a[1].y - a[3].y);
+  a[0] = make_float2(t0.x + t2.x, t0.y + t2.y);
+  const float2 y2 = make_float2(t0.x - t2.x, t0.y - t2.y);
+  const float2 y1 = make_float2(t1.x + t3.y, t1.y - t3.x);  // t1 - i t3
+  const float2 y3 = make_float2(t1.x - t3.y, t1.y + t3.x);  // t1 + i t3
+  a[1] = twiddle ? cmul(y1, w[0]) : y1;
+  a[2] = twiddle ? cmul(y2, w[1]) : y2;
+  a[3] = twiddle ? cmul(y3, w[2]) : y3;
+}
+
+CASR_DEV void lds_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
 
 __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ wav,
                                                       const int32_t* __restrict__ nsamp, int Nmax,
                                                       int Tmax, float pre, const FrontendConst* __restrict__ k,
                                                       float* __restrict__ out, int32_t* __restrict__ frames,
                                                       int32_t* __restrict__ err) {
-  __shared__ double zr[FPB][NC], zi[FPB][NC];
-  __shared__ float pw[FPB][NBIN + 3];
+  __shared__ float2 zs[FE_WAVES][NC];
+  __shared__ float pw[FE_WAVES][NBIN + 3];
+  __shared__ float fbs[F][FE_FBW + 1];  // the filters' nonzero weights (+1: lanes m read conflict-free)
+  __shared__ int lohi[2][F];
   const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int f = blockIdx.x * FPB + w;
+  for (int i = threadIdx.x; i < F * FE_FBW; i += blockDim.x) fbs[i / FE_FBW][i % FE_FBW] = (&k->fb[0][0])[i];
+  for (int i = threadIdx.x; i < F; i += blockDim.x) {
+    lohi[0][i] = k->lo[i];
+    lohi[1][i] = k->hi[i];
+  }
+  __syncthreads();  // the only block barrier: the waves run their frames independently after it
   int n = nsamp[b];
   if (n < NFFT + 1 || n > Nmax) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err, CASR_DEV_BAD_AUDIO);
@@ -58,62 +94,118 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
   }
   const int L = n - 1 >= NFFT ? 1 + (n - 1 - NFFT) / HOP : 0;  // frames of the pre-emphasised signal
   if (blockIdx.x == 0 && threadIdx.x == 0) frames[b] = L < Tmax ? L : Tmax;
-  // every wave runs through every barrier; only frames f < min(L, Tmax) read samples
-  const bool live = f < L && f < Tmax;
-  const float* x = wav + (size_t)b * Nmax + (size_t)(live ? f : 0) * HOP;
-  // windowed frame, complex-packed and bit-reversed: z[m] = (y[2m] w[2m], y[2m+1] w[2m+1])
+  const int f0 = (blockIdx.x * FE_WAVES + w) * FE_FPW;
+  if (f0 >= Tmax) return;  // no block barrier below: the waves are independent
+  // per-lane constants of every frame: window values of the lane's 8 samples, the twiddles of the
+  // three twiddled stages (group offset j of the lane: lane, lane & 15, lane & 3), the split twiddles
+  float wn[4][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = lane + 64 * i, j0 = 2 * m, j1 = j0 + 1;
-    float v0 = 0.f, v1 = 0.f;
-    if (live && j0 >= LPAD && j0 < LPAD + WIN)
-      v0 = preemph_win(k->win[j0 - LPAD], x[j0 + 1], x[j0], pre);
-    if (live && j1 >= LPAD && j1 < LPAD + WIN)
-      v1 = preemph_win(k->win[j1 - LPAD], x[j1 + 1], x[j1], pre);
-    const int r = bitrev8(m);
-    zr[w][r] = v0;
-    zi[w][r] = v1;
-  }
-  __syncthreads();
-  // 8 radix-2 DIT stages, 128 butterflies each: 2 per lane
+  for (int r = 0; r < 4; ++r)
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int half = 1 << s;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int t = lane + 64 * i, pos = t & (half - 1);
-      const int i0 = ((t >> s) << (s + 1)) + pos, i1 = i0 + half;
-      const double wr = k->tw256r[pos << (7 - s)], wi = k->tw256i[pos << (7 - s)];
-      const double br = zr[w][i1] * wr - zi[w][i1] * wi, bi = zr[w][i1] * wi + zi[w][i1] * wr;
-      const double ar = zr[w][i0], ai = zi[w][i0];
-      zr[w][i0] = ar + br;
-      zi[w][i0] = ai + bi;
-      zr[w][i1] = ar - br;
-      zi[w][i1] = ai - bi;
+    for (int e = 0; e < 2; ++e) {
+      const int j = 2 * (lane + 64 * r) + e;
+      wn[r][e] = (j >= LPAD && j < LPAD + WIN) ? k->win[j - LPAD] : 0.f;
     }
-    __syncthreads();
+  float2 tw[3][3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int j = lane & (63 >> (2 * s)), step = 1 << (2 * s);  // W_{256 / step}^{j q} = W_256^{step j q}
+#pragma unroll
+    for (int q = 1; q <= 3; ++q) {
+      const int i = (step * j * q) & (NC - 1);
+      tw[s][q - 1] = make_float2(k->tw256r[i], k->tw256i[i]);
+    }
   }
-  // real-input split: X[q] = E + W512^q O, E = (Z[q] + conj Z[-q]) / 2, O = (Z[q] - conj Z[-q]) / 2i
-  for (int q = lane; q < NBIN; q += 64) {
-    const int qa = q & (NC - 1), qb = (NC - q) & (NC - 1);
-    const double zr1 = zr[w][qa], zi1 = zi[w][qa], zr2 = zr[w][qb], zi2 = -zi[w][qb];
-    const double er = 0.5 * (zr1 + zr2), ei = 0.5 * (zi1 + zi2);
-    const double orr = 0.5 * (zi1 - zi2), oi = -0.5 * (zr1 - zr2);
-    const double c = k->tw512r[q], sn = k->tw512i[q];
-    const float xr = (float)(er + (orr * c - oi * sn)), xi = (float)(ei + (orr * sn + oi * c));
-    pw[w][q] = power2(xr, xi);
+  float2 t512[5];
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {
+    const int q = min(lane + 64 * r, NBIN - 1);
+    t512[r] = make_float2(k->tw512r[q], k->tw512i[q]);
   }
-  __syncthreads();
-  if (f >= Tmax) return;
-  float* o = out + ((size_t)b * Tmax + f) * F;
-  for (int m = lane; m < F; m += 64) {
-    if (!live) {  // padding rows past the utterance
-      o[m] = 0.f;
+  const int nmel = lane + 64 < F ? 2 : 1;
+  // the samples of a frame: point m = lane + 64 r needs x[2m .. 2m + 2] (pre-emphasis reads the next
+  // sample); loaded one frame ahead, so a frame's loads fly while the previous frame computes
+  float xs[4][3];
+  auto load_frame = [&](int f) {
+    const bool live = f < L && f < Tmax;
+    const float* x = wav + (size_t)b * Nmax + (size_t)(live ? f : 0) * HOP;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 2 * (lane + 64 * r);
+      const bool in = live && j + 1 >= LPAD && j < LPAD + WIN;  // a window value of the pair is nonzero
+#pragma unroll
+      for (int e = 0; e < 3; ++e) xs[r][e] = in ? x[j + e] : 0.f;
+    }
+  };
+  load_frame(f0);
+  for (int fi = 0; fi < FE_FPW; ++fi) {
+    const int f = f0 + fi;
+    if (f >= Tmax) break;
+    float* o = out + ((size_t)b * Tmax + f) * F;
+    if (f >= L) {  // padding rows past the utterance (wave-uniform)
+      for (int m = lane; m < F; m += 64) o[m] = 0.f;
       continue;
     }
-    float acc = 0.f;
-    for (int q = k->lo[m]; q < k->hi[m]; ++q) acc = fmaf(pw[w][q], k->fb[q * F + m], acc);  // matmul: fused
-    o[m] = logf(acc == 0.f ? 1.1920928955078125e-07f : acc);
+    float2 a[4];
+    // windowed, pre-emphasised frame: point m = lane + 64 r is (y[2m] w, y[2m+1] w)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      a[r] = make_float2(preemph_win(wn[r][0], xs[r][1], xs[r][0], pre), preemph_win(wn[r][1], xs[r][2], xs[r][1], pre));
+    if (fi + 1 < FE_FPW) load_frame(f + 1);
+    // stage 0 (S = 64): the lane's points are its butterfly
+    bfly4(a, tw[0], true);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zs[w][fe_slot(lane + 64 * q)] = a[q];
+    lds_fence();
+    // stage 1 (S = 16): group lane >> 4, offset lane & 15
+    {
+      const int base = 64 * (lane >> 4) + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = zs[w][fe_slot(base + 16 * r)];
+      bfly4(a, tw[1], true);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zs[w][fe_slot(base + 16 * q)] = a[q];
+    }
+    lds_fence();
+    {  // stage 2 (S = 4): group lane >> 2, offset lane & 3
+      const int base = 16 * (lane >> 2) + (lane & 3);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = zs[w][fe_slot(base + 4 * r)];
+      bfly4(a, tw[2], true);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zs[w][fe_slot(base + 4 * q)] = a[q];
+    }
+    lds_fence();
+    {  // stage 3 (S = 1): group lane, no twiddle
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] = zs[w][fe_slot(4 * lane + r)];
+      bfly4(a, tw[0], false);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zs[w][fe_slot(4 * lane + q)] = a[q];
+    }
+    lds_fence();
+    // real-input split: X[q] = E + W512^q O, E = (Z[q] + conj Z[-q]) / 2, O = (Z[q] - conj Z[-q]) / 2i
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const int q = lane + 64 * r;
+      if (q < NBIN) {
+        const float2 z1 = zs[w][fe_slot(rev4(q & (NC - 1)))], z2 = zs[w][fe_slot(rev4((NC - q) & (NC - 1)))];
+        const float er = 0.5f * (z1.x + z2.x), ei = 0.5f * (z1.y - z2.y);
+        const float orr = 0.5f * (z1.y + z2.y), oi = -0.5f * (z1.x - z2.x);
+        const float c = t512[r].x, sn = t512[r].y;
+        pw[w][q] = power2(er + (orr * c - oi * sn), ei + (orr * sn + oi * c));
+      }
+    }
+    lds_fence();
+    // mel projection (a float32 fma chain over the filter's nonzero bins, in bin order) and log
+    for (int u = 0; u < nmel; ++u) {
+      const int m = lane + 64 * u;
+      const int lo = lohi[0][m], nz = lohi[1][m] - lo;
+      float acc = 0.f;
+      for (int i = 0; i < nz; ++i) acc = fmaf(pw[w][lo + i], fbs[m][i], acc);  // matmul: fused
+      o[m] = logf(acc == 0.f ? 1.1920928955078125e-07f : acc);
+    }
+    lds_fence();  // this frame's pw / zs reads are done before the next frame's writes
   }
 }
 }  // namespace
@@ -144,9 +236,9 @@ void mel_filterbank(int n_stft, float f_min, float f_max, int n_mels, float* fb)
 }
 
 void build_frontend_const(FrontendConst* c) {
-  float fb[NBIN * F];
-  mel_filterbank(NBIN, 80.f, 7600.f, F, fb);
-  for (int i = 0; i < NBIN * F; ++i) c->fb[i] = fb[i];
+  std::vector<float> fb(NBIN * F);
+  mel_filterbank(NBIN, 80.f, 7600.f, F, fb.data());
+  *c = FrontendConst{};
   for (int m = 0; m < F; ++m) {
     int lo = NBIN, hi = 0;
     for (int q = 0; q < NBIN; ++q)
@@ -154,18 +246,21 @@ void build_frontend_const(FrontendConst* c) {
         lo = q < lo ? q : lo;
         hi = q + 1;
       }
-    c->lo[m] = lo < hi ? lo : 0;
-    c->hi[m] = lo < hi ? hi : 0;
+    if (lo >= hi) lo = hi = 0;
+    if (hi - lo > FE_FBW) hi = lo + FE_FBW;  // not reached: the widest filter has 17 bins
+    c->lo[m] = lo;
+    c->hi[m] = hi;
+    for (int q = lo; q < hi; ++q) c->fb[m][q - lo] = fb[q * F + m];
   }
   // torch.hann_window(400) (periodic): 0.5 - 0.5 cos(2 pi j / 400), evaluated in float32
   for (int j = 0; j < WIN; ++j) c->win[j] = (float)(0.5 - 0.5 * cos(2.0 * M_PI * j / WIN));
-  for (int i = 0; i < NC / 2; ++i) {
-    c->tw256r[i] = cos(-2.0 * M_PI * i / NC);
-    c->tw256i[i] = sin(-2.0 * M_PI * i / NC);
+  for (int i = 0; i < NC; ++i) {
+    c->tw256r[i] = (float)cos(-2.0 * M_PI * i / NC);
+    c->tw256i[i] = (float)sin(-2.0 * M_PI * i / NC);
   }
   for (int q = 0; q < NBIN; ++q) {
-    c->tw512r[q] = cos(-2.0 * M_PI * q / NFFT);
-    c->tw512i[q] = sin(-2.0 * M_PI * q / NFFT);
+    c->tw512r[q] = (float)cos(-2.0 * M_PI * q / NFFT);
+    c->tw512i[q] = (float)sin(-2.0 * M_PI * q / NFFT);
   }
 }
 
@@ -175,6 +270,7 @@ int frontend_frames(int n_samples) {
 
 hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nmax, int Tmax, float pre,
                           const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s) {
+  constexpr int FPB = FE_WAVES * FE_FPW;  // frames per block
   dim3 grid((Tmax + FPB - 1) / FPB > 0 ? (Tmax + FPB - 1) / FPB : 1, B);
   hipLaunchKernelGGL(log_mel_kernel, grid, dim3(256), 0, s, wav, nsamp, Nmax, Tmax, pre, k, out, frames, err);
   return hipGetLastError();

@@ -245,7 +245,21 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            0: three launches per step (LSTMCell GEMM, attention, projection).
  *                            Replaces decoder.py:104-114 + attention.py:92 + decoder.py:129-135 per
  *                            step with the same arithmetic regrouped (gates = [ctx | h] W_ch^T +
- *                            (emb W_emb^T + b), q by f32 fma chains) */
+ *                            (emb W_emb^T + b), q by f32 fma chains).  It is also the default beam
+ *                            step at R = B k >= 1024 decode rows when the attention takes 4 or 8 beam
+ *                            rows per block and every projection and decoder LSTM weight is below 16
+ *                            in magnitude (blob info words 4 and 5): there the fused GEMM runs the
+ *                            one-accumulator s16x3 form (the whole sum scaled by 2^11) and the beam
+ *                            attention kernel applies the cell (CELL 2).  Same token ids as the
+ *                            three-launch step; scores within 2e-3, alignments within 1e-5
+ *                            (tests/test_gpu_parity.py test_decode_fold_vs_three_launches,
+ *                            test_beam_fold_vs_three_launches).  Not used by casr_beam at k = 1.
+ * One option exists for tests only:
+ *   CASR_OPT_REC_COOP_REFUSE 0 (default): off; n in 1..8: casr_encode treats the cooperative launch
+ *                            of encoder layer n - 1 as refused (hipErrorCooperativeLaunchTooLarge,
+ *                            without launching), so the mid-encode fallback to the per-step
+ *                            recurrence (that layer and every later one) can be checked bit for bit
+ *                            against all-persistent and all-per-step encodes */
 enum {
   CASR_OPT_FUSE_SELECT = 0,
   CASR_OPT_REC_LAYOUT = 1,
@@ -258,7 +272,8 @@ enum {
   CASR_OPT_ATTN_KPB = 8,
   CASR_OPT_ATTN_DIRECT = 9,
   CASR_OPT_DEC_FOLD = 10,
-  CASR_OPT_COUNT = 11
+  CASR_OPT_REC_COOP_REFUSE = 11,
+  CASR_OPT_COUNT = 12
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

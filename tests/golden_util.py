@@ -67,3 +67,27 @@ def near_tie_beam_check(tokens, score, gold, atol, rescore=None, atol_same=None,
         if rescore is not None:
             assert abs(rescore(b, gold["tokens"][b]) - gs[b]) <= atol_same, b
             assert abs(rescore(b, list(tokens[b])) - score[b]) <= atol_same, b
+
+
+def near_tie_records_check(mine, gold, atol, rescore=None):
+    """Finished-hypothesis records of one utterance (parse_finished_tensors order: step, then
+    rank; each (tokens, score)) against the oracle's.  Returns True when the lists are identical
+    (tokens equal, scores within ``atol``), False when they diverge at a near-tied pruning
+    decision, which is accepted only when:
+      * every record before the first differing one is identical (tokens, scores within atol);
+      * the two diverging records are genuine hypotheses: with ``rescore(tokens) -> oracle
+        log-probability of tokens + EOS`` (teacher-forced), ours re-scores to our score and the
+        oracle's to the oracle's, each within ``atol``.
+    So both searches kept correctly scored hypotheses and split only where f32 summation order
+    can reorder candidates of (near-)equal score (the same rule as near_tie_beam_check)."""
+    n = min(len(mine), len(gold))
+    d = next((i for i in range(n) if list(mine[i][0]) != list(gold[i][0])), None)
+    if d is None and len(mine) == len(gold):
+        np.testing.assert_allclose([x[1] for x in mine], [x[1] for x in gold], rtol=0, atol=atol)
+        return True
+    d = n if d is None else d
+    np.testing.assert_allclose([x[1] for x in mine[:d]], [x[1] for x in gold[:d]], rtol=0, atol=atol)
+    assert rescore is not None, "records diverge and no rescoring was given"
+    for rec in (mine[d:d + 1] + gold[d:d + 1]):
+        assert abs(rescore(list(rec[0])) - rec[1]) <= atol, (d, rec)
+    return False

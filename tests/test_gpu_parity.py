@@ -307,6 +307,50 @@ def test_persistent_recurrence_equals_per_step(eng, B, layout):
             assert torch.equal(a, b)
 
 
+def test_cooperative_refusal_mid_encode_falls_back_bitwise(eng):
+    """A refused cooperative launch (hipErrorCooperativeLaunchTooLarge: the grid cannot be
+    co-resident) switches that layer and every later one to the per-step recurrence, and zeroes
+    their outputs first (casr_capi.hip encode_impl).  Forced through CASR_OPT_REC_COOP_REFUSE at
+    layer 0, 1 and 3 (the last: the keys then come from the fallback's split image): encoder
+    outputs, final states, keys and greedy / beam tokens bitwise equal to an all-persistent and to
+    an all-per-step encode, ragged lengths (B = 48)."""
+    B = 48
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    rs = np.random.RandomState(23)
+    frames = rs.randint(9, 601, size=B)
+    frames[0] = 600
+    x = np.zeros((B, 600, 80), np.float32)
+    for b in range(B):
+        x[b, :frames[b]] = fbank_for(b, int(frames[b]))
+    feat, flen = eng.features(torch.from_numpy(x).to(eng.device),
+                              torch.from_numpy(frames.astype(np.int32)).to(eng.device))
+
+    def run():
+        eng.encode(feat, flen)
+        res = [t.cpu() for t in eng.encoder_results()]
+        res.append(eng.greedy()["tokens"].cpu())
+        res.append(eng.beam(4)["tokens"].cpu())
+        assert eng.device_flags() == 0
+        return res
+
+    outs = {}
+    try:
+        outs["persistent"] = run()
+        eng.set_persistent(False)
+        outs["per_step"] = run()
+        eng.set_persistent(True)
+        for layer in (0, 1, 3):
+            eng.set_option("REC_COOP_REFUSE", layer + 1)
+            outs[f"refused_{layer}"] = run()
+    finally:
+        eng.set_option("REC_COOP_REFUSE", 0)
+        eng.set_persistent(True)
+    for name, got in outs.items():
+        for i, (a, b) in enumerate(zip(outs["persistent"], got)):
+            assert torch.equal(a, b), (name, i)
+
+
 def test_recurrence_pacing_options_bitwise(eng):
     """The recurrence's pacing options (first-poll sleep, second-poll gap) change only when a
     workgroup looks at its producers' words, never what it computes: encoder results bitwise equal
@@ -404,8 +448,8 @@ def test_batch_invariance_and_determinism(eng):
     t2 = eng.beam(8)["tokens"].cpu()
     assert torch.equal(t1[:16], t2)
     # k = 16: 64 x 16 = 1024 rows (the 128 x 160 projection blocks) against 8 x 16 = 128 rows (the
-    # 64 x 80 ones); both take the tile-maxima threshold at temperature 1 (the lanes' top-2 bound
-    # is covered by test_beam_select_threshold_paths_bitwise)
+    # 64 x 80 ones); both take the tile-maxima threshold at temperature 1 (the select path over
+    # full logit rows, T != 1, is covered by test_beam_temperature_matches_reference)
     eng.encode(feat[:64].contiguous(), flen[:64].contiguous())
     t3 = eng.beam(16)["tokens"].cpu()
     assert eng.device_flags() == 0
