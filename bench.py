@@ -417,8 +417,13 @@ def main():
 
         step_small()
         dts = timed(step_small, args.steps, "config2")
+        eng.profile(CLASSES)  # one instrumented step: where a B = 32 batch spends its time
+        step_small()
+        bds = eng.profile_read()
+        eng.profile([])
         small = {"config": "BASELINE config 2: greedy, B=32/GPU, T=800", "batch_per_gpu": Bs,
                  "device_ms_per_step": step_stats("config2"),
+                 "kernel_breakdown_ms": {c: round(v[1], 3) for c, v in bds.items()},
                  "value": Bs * world * args.steps / dts, "unit": "utt/s", "ms_per_step": 1000.0 * dts / args.steps}
 
     # BASELINE config 1: one 8 s WAV, greedy, through the drop-in main.parse (main.py:27-65):

@@ -143,19 +143,23 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   // cell phase, which it does not depend on, so the scores start on landed keys
   constexpr bool PRE = CELL == 1 || (CELL == 2 && KPB >= 8);  // (KPB 4: 20 keys rows per batch, no registers left)
   float4 kvp[PRE ? CH : 1];
-  if constexpr (PRE) {
+  auto preload_keys = [&]() {
     const int ag = tid / nch, t0 = 4 * (tid - ag * nch), a0 = ag * apg, a1 = min(A, a0 + apg);
     const bool live = !direct && tid < G * nch && t0 < len;
 #pragma unroll
     for (int i = 0; i < CH; ++i)
       kvp[i] = live && a0 + i < a1 ? *reinterpret_cast<const float4*>(ekb + (size_t)(a0 + i) * Tq + t0)
                                    : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+  };
+  if constexpr (PRE && CELL != 1) preload_keys();
   if constexpr (CELL == 1) {
     // 0. the folded step's LSTM cell (decoder.py:104-114) and query (attention.py:92) for row r.
-    // The previous step's gate pre-activations of unit u = tid and its c are loaded first (with the
-    // keys above and the select's partials: none depends on the select); the W_hidden slice (rows
-    // 32 us .. +31, columns 4 a4 .. +3) with the token's gate-table row, after the select
+    // Load order (round 4): a wave's loads retire in issue order, so whatever a wave issues first is
+    // what it waits on first.  Wave 0 issues the select's partials before anything else (they were
+    // queued behind the block's whole keys batch, ~136 KB, before); the previous step's gate
+    // pre-activations of unit u = tid and its c and the W_hidden slice (rows 32 us .. +31, columns
+    // 4 a4 .. +3) follow; after the select, the token's gate-table row, then the first keys batch:
+    // the keys stream in under the cell and the query
     __shared__ int tk_s, skip_s;
     const int r = (int)row0;
     const int a4 = tid & (A / 4 - 1), us = tid / (A / 4);
@@ -163,9 +167,26 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     const int u = tid;
     auto gcol = [](int g, int u) { return (u >> 4) * 64 + g * 16 + (u & 15); };  // packed_gate_row
     float gprev[4];
+    float cold;
+    auto load_prev = [&]() {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) gprev[g] = cell.gates[(size_t)r * (4 * HD) + gcol(g, u)];
-    const float cold = cell.st_old[(size_t)r * ST + C + HD + u];
+      for (int g = 0; g < 4; ++g) gprev[g] = cell.gates[(size_t)r * (4 * HD) + gcol(g, u)];
+      cold = cell.st_old[(size_t)r * ST + C + HD + u];
+    };
+    // the W_hidden slice (256 KB per block, L2-resident) is the prologue's largest read: issued at
+    // the start (wave 0: right after the select's own loads), it lands under the select and the
+    // gate-row gather instead of after them (round 4: prologue 9.4 us p50 with it issued after the
+    // select)
+    float4 wh[UPS];
+    auto load_wh = [&]() {
+#pragma unroll
+      for (int i = 0; i < UPS; ++i)
+        wh[i] = *reinterpret_cast<const float4*>(cell.w_hidden + (size_t)(UPS * us + i) * A + 4 * a4);
+    };
+    if (wv != 0) {
+      load_prev();
+      load_wh();
+    }
     if (wv == 0) {  // the select of step l - 1 (greedy_select_part_kernel's arithmetic) and its bookkeeping
       // rows finished before step l - 1 (the select's own skip) and before step l (the block's early
       // exit), from one load of the counters issued with the partials: the second misses what this
@@ -183,6 +204,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
           se = gs.gp.se[(size_t)r * GP_NB + ln];
           mi = gs.gp.ix[(size_t)r * GP_NB + ln];
         }
+        load_wh();
         uint8_t fin0 = 0;
         float acc0 = 0.f;
         int len0 = 0;
@@ -206,6 +228,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
         }
       } else {
         t = cell.tok[r];
+        load_wh();
         if ((unsigned)t >= (unsigned)V) {
           if (ln == 0) atomicOr(cell.err, CASR_DEV_BAD_TOKEN);
           t = 0;
@@ -215,17 +238,16 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
         tk_s = t;
         skip_s = dn >= total;
       }
+      load_prev();
     }
     __syncthreads();
+    stamp(6);  // (diagnostics) the select and its bookkeeping done
     if (skip_s) return;
     const int t = tk_s;
     float eg[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) eg[g] = cell.emb_gates[(size_t)t * (4 * HD) + gcol(g, u)];
-    float4 wh[UPS];
-#pragma unroll
-    for (int i = 0; i < UPS; ++i)
-      wh[i] = *reinterpret_cast<const float4*>(cell.w_hidden + (size_t)(UPS * us + i) * A + 4 * a4);
+    preload_keys();
     float h2, c2;
     lstm_cell_hw(gprev[0] + eg[0], gprev[1] + eg[1], gprev[2] + eg[2], gprev[3] + eg[3], cold, h2, c2);
     st[(size_t)r * ST + C + u] = h2;
@@ -233,6 +255,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     reinterpret_cast<uint32_t*>(st)[(size_t)r * ST + ST16 + C + u] = split16_word(h2);
     hs[u] = h2;
     __syncthreads();
+    stamp(7);  // (diagnostics) the cell done, h in LDS
     float4 qa = make_float4(0.f, 0.f, 0.f, 0.f);  // units in order within the slice
 #pragma unroll
     for (int i = 0; i < UPS; ++i) {

@@ -190,7 +190,7 @@ struct CopyList {
 hipError_t copy_multi(const CopyList& cl, hipStream_t s);
 
 // frontend.hip: wav -> log-mel.  Constant tables live in one device struct per handle.
-constexpr int FE_FBW = 32;  // widest mel filter kept (nonzero bins; the widest has 17)
+constexpr int FE_FBW = 20;  // widest mel filter kept (nonzero bins; the widest has 17)
 struct FrontendConst {
   float fb[F][FE_FBW];          // filter m's nonzero weights, bins lo[m] .. hi[m] - 1
   int32_t lo[F], hi[F];         // nonzero bin range of each mel filter

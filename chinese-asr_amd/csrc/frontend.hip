@@ -18,8 +18,10 @@
 // same for every frame and stay in registers.  Power and the mel projection are float32 like the
 // reference.  Frames past an utterance's length are written as zeros.  The constant tables
 // (per-filter nonzero weights, window, twiddles rounded once from double) are built on the host.
+#include <assert.h>
 #include <math.h>
 
+#include <type_traits>
 #include <vector>
 
 #include "casr_common.h"
@@ -32,6 +34,7 @@ constexpr int NFFT = 512, HOP = 160, WIN = 400, LPAD = (NFFT - WIN) / 2, NBIN = 
 constexpr int NC = NFFT / 2;  // complex FFT size
 constexpr int FE_WAVES = 4;   // waves (frames in flight) per block
 constexpr int FE_FPW = 8;     // consecutive frames per wave
+constexpr int FE_W0 = 10, FE_W1 = 17;  // widest of mel filters 0..63 / 64..79 (build_frontend_const checks)
 
 // torch's elementwise steps, each rounded (no FMA contraction: hipcc's default would fuse them):
 // pre-emphasis x[t+1] - 0.97 x[t] (data.py:201-202), the window product, |X|^2 = re^2 + im^2
@@ -80,8 +83,12 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
   __shared__ float pw[FE_WAVES][NBIN + 3];
   __shared__ float fbs[F][FE_FBW + 1];  // the filters' nonzero weights (+1: lanes m read conflict-free)
   __shared__ int lohi[2][F];
+  __shared__ float2 t256[NC], t512s[NBIN];  // twiddles (read per frame with the stage's data: registers
+                                           // for a fourth wave per SIMD)
   const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < F * FE_FBW; i += blockDim.x) fbs[i / FE_FBW][i % FE_FBW] = (&k->fb[0][0])[i];
+  for (int i = threadIdx.x; i < NC; i += blockDim.x) t256[i] = make_float2(k->tw256r[i], k->tw256i[i]);
+  for (int i = threadIdx.x; i < NBIN; i += blockDim.x) t512s[i] = make_float2(k->tw512r[i], k->tw512i[i]);
   for (int i = threadIdx.x; i < F; i += blockDim.x) {
     lohi[0][i] = k->lo[i];
     lohi[1][i] = k->hi[i];
@@ -106,23 +113,12 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
       const int j = 2 * (lane + 64 * r) + e;
       wn[r][e] = (j >= LPAD && j < LPAD + WIN) ? k->win[j - LPAD] : 0.f;
     }
-  float2 tw[3][3];
+  // stage s's twiddles of this lane: W_{256 / step}^{j q} = W_256^{step j q}, j = lane & (63 >> 2s)
+  auto twiddles = [&](int s, float2 (&tw)[3]) {
+    const int j = lane & (63 >> (2 * s)), step = 1 << (2 * s);
 #pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    const int j = lane & (63 >> (2 * s)), step = 1 << (2 * s);  // W_{256 / step}^{j q} = W_256^{step j q}
-#pragma unroll
-    for (int q = 1; q <= 3; ++q) {
-      const int i = (step * j * q) & (NC - 1);
-      tw[s][q - 1] = make_float2(k->tw256r[i], k->tw256i[i]);
-    }
-  }
-  float2 t512[5];
-#pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int q = min(lane + 64 * r, NBIN - 1);
-    t512[r] = make_float2(k->tw512r[q], k->tw512i[q]);
-  }
-  const int nmel = lane + 64 < F ? 2 : 1;
+    for (int q = 1; q <= 3; ++q) tw[q - 1] = t256[(step * j * q) & (NC - 1)];
+  };
   // the samples of a frame: point m = lane + 64 r needs x[2m .. 2m + 2] (pre-emphasis reads the next
   // sample); loaded one frame ahead, so a frame's loads fly while the previous frame computes
   float xs[4][3];
@@ -153,7 +149,9 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
       a[r] = make_float2(preemph_win(wn[r][0], xs[r][1], xs[r][0], pre), preemph_win(wn[r][1], xs[r][2], xs[r][1], pre));
     if (fi + 1 < FE_FPW) load_frame(f + 1);
     // stage 0 (S = 64): the lane's points are its butterfly
-    bfly4(a, tw[0], true);
+    float2 tw[3];
+    twiddles(0, tw);
+    bfly4(a, tw, true);
 #pragma unroll
     for (int q = 0; q < 4; ++q) zs[w][fe_slot(lane + 64 * q)] = a[q];
     lds_fence();
@@ -162,7 +160,8 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
       const int base = 64 * (lane >> 4) + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) a[r] = zs[w][fe_slot(base + 16 * r)];
-      bfly4(a, tw[1], true);
+      twiddles(1, tw);
+      bfly4(a, tw, true);
 #pragma unroll
       for (int q = 0; q < 4; ++q) zs[w][fe_slot(base + 16 * q)] = a[q];
     }
@@ -171,7 +170,8 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
       const int base = 16 * (lane >> 2) + (lane & 3);
 #pragma unroll
       for (int r = 0; r < 4; ++r) a[r] = zs[w][fe_slot(base + 4 * r)];
-      bfly4(a, tw[2], true);
+      twiddles(2, tw);
+      bfly4(a, tw, true);
 #pragma unroll
       for (int q = 0; q < 4; ++q) zs[w][fe_slot(base + 4 * q)] = a[q];
     }
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
     {  // stage 3 (S = 1): group lane, no twiddle
 #pragma unroll
       for (int r = 0; r < 4; ++r) a[r] = zs[w][fe_slot(4 * lane + r)];
-      bfly4(a, tw[0], false);
+      bfly4(a, tw, false);
 #pragma unroll
       for (int q = 0; q < 4; ++q) zs[w][fe_slot(4 * lane + q)] = a[q];
     }
@@ -192,19 +192,33 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
         const float2 z1 = zs[w][fe_slot(rev4(q & (NC - 1)))], z2 = zs[w][fe_slot(rev4((NC - q) & (NC - 1)))];
         const float er = 0.5f * (z1.x + z2.x), ei = 0.5f * (z1.y - z2.y);
         const float orr = 0.5f * (z1.y + z2.y), oi = -0.5f * (z1.x - z2.x);
-        const float c = t512[r].x, sn = t512[r].y;
+        const float2 tq = t512s[q];
+        const float c = tq.x, sn = tq.y;
         pw[w][q] = power2(er + (orr * c - oi * sn), ei + (orr * sn + oi * c));
       }
     }
     lds_fence();
-    // mel projection (a float32 fma chain over the filter's nonzero bins, in bin order) and log
-    for (int u = 0; u < nmel; ++u) {
-      const int m = lane + 64 * u;
-      const int lo = lohi[0][m], nz = lohi[1][m] - lo;
+    // mel projection (a float32 fma chain over the filter's nonzero bins, in bin order) and log.
+    // Fixed trip counts, every LDS read of a pass issued before its fma chain: pass 0 = filters
+    // 0..63 (at most FE_W0 bins), pass 1 = filters 64..79 on lanes 0..15 (at most FE_W1 bins).  The
+    // weights past a filter's last bin are zero (fma(x, 0, acc) = acc for the finite powers; a
+    // non-finite power makes the sum NaN, as the reference's full-length matmul does)
+    auto mel = [&](auto NW, int m) {
+      constexpr int W = decltype(NW)::value;
+      const int lo = lohi[0][m];
+      float pv[W], wv[W];
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        pv[i] = pw[w][min(lo + i, NBIN - 1)];
+        wv[i] = fbs[m][i];
+      }
       float acc = 0.f;
-      for (int i = 0; i < nz; ++i) acc = fmaf(pw[w][lo + i], fbs[m][i], acc);  // matmul: fused
+#pragma unroll
+      for (int i = 0; i < W; ++i) acc = fmaf(pv[i], wv[i], acc);  // matmul: fused
       o[m] = logf(acc == 0.f ? 1.1920928955078125e-07f : acc);
-    }
+    };
+    mel(std::integral_constant<int, FE_W0>{}, lane);
+    if (lane + 64 < F) mel(std::integral_constant<int, FE_W1>{}, lane + 64);
     lds_fence();  // this frame's pw / zs reads are done before the next frame's writes
   }
 }
@@ -247,7 +261,11 @@ void build_frontend_const(FrontendConst* c) {
         hi = q + 1;
       }
     if (lo >= hi) lo = hi = 0;
-    if (hi - lo > FE_FBW) hi = lo + FE_FBW;  // not reached: the widest filter has 17 bins
+    // the kernel's fixed trip counts (FE_W0 / FE_W1 bins): not exceeded by this filterbank (widest 10 /
+    // 17); a wider filter would be truncated, so fail loudly in a debug build
+    const int wmax = m < 64 ? FE_W0 : FE_W1;
+    assert(hi - lo <= wmax);
+    if (hi - lo > wmax) hi = lo + wmax;
     c->lo[m] = lo;
     c->hi[m] = hi;
     for (int q = lo; q < hi; ++q) c->fb[m][q - lo] = fb[q * F + m];

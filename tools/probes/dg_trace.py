@@ -29,6 +29,11 @@ def attn_report(r, title):
         print(f"  {n:14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
     v = t[:, 0]
     print(f"  {'start':14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
+    if (r[:, 6] > 0).all() and (r[:, 7] > 0).all():  # the folded step's prologue (CELL 1 stamps 6, 7)
+        t6 = (r[:, 6] - r[:, 0].min()) * 10 / 1000.0
+        t7 = (r[:, 7] - r[:, 0].min()) * 10 / 1000.0
+        for n, v in (("  select", t6 - t[:, 0]), ("  cell", t7 - t6), ("  query", t[:, 1] - t7)):
+            print(f"  {n:14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
 def gemm_report(raw, tag):
     for cls, name in ((0, "dec_lstm"), (1, "proj")):
         r = raw[cls]
