@@ -128,7 +128,10 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   float* vl = hs + (CELL == 1 ? AT_CELL_FLOATS : 0);  // [npf][C]: value rows 0..npf-1 (LDS-DMA)
   const int b = blockIdx.x, j0 = blockIdx.y * KPB;
   const int nk = min(KPB, k - j0);
-  const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
+  // CELL 1: wv through readfirstlane, provably wave-uniform, so the prologue's per-wave roles are
+  // scalar branches (blocks of their own for hipcc's wait insertion, not exec-masked regions whose
+  // pending loads merge); the other instances keep the plain form (their register allocation)
+  const int tid = threadIdx.x, wv = CELL == 1 ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6, ln = tid & 63;
   const int len = min(lens[b], Tp);
   const size_t row0 = (size_t)b * k + j0;
 
@@ -183,36 +186,46 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       for (int i = 0; i < UPS; ++i)
         wh[i] = *reinterpret_cast<const float4*>(cell.w_hidden + (size_t)(UPS * us + i) * A + 4 * a4);
     };
-    if (wv != 0) {
-      load_prev();
-      load_wh();
-    }
     if (wv == 0) {  // the select of step l - 1 (greedy_select_part_kernel's arithmetic) and its bookkeeping
       // rows finished before step l - 1 (the select's own skip) and before step l (the block's early
       // exit), from one load of the counters issued with the partials: the second misses what this
       // launch's selects add to step l - 1, so a block that sees every row finished skips work nothing
-      // downstream reads, and one that does not computes it
+      // downstream reads, and one that does not computes it.
+      // (round 4) Every operand load of the select is issued before its first use, in straight-line
+      // code (clamped indices and selects instead of lane-masked regions, the sel branch on a kernel
+      // argument), then the W_hidden slice: one round trip before the select instead of two, and no
+      // wait of hipcc's between the loads (masked regions made it drain the counters' load before
+      // the partials' and the partials' before W_hidden's)
+      const GreedySel& gs = cell.gs;
+      const int lm = max(gs.lsel, l);  // 1 ..max_len, at most 64 (prepare_decode: the fold needs it)
+      const int cnt = newdone[min(ln, lm - 1)];
+      const int pi = r * GP_NB + min(ln, max(gs.nbp - 1, 0));
+      float m = 0.f, se = 0.f;
+      int mi = 0, tq = 0, bkv = 0;
+      if (cell.sel) {
+        m = gs.gp.mx[pi];
+        se = gs.gp.se[pi];
+        mi = gs.gp.ix[pi];
+        // the row's bookkeeping words in lanes 0..2 of one load: the dword holding fin[r], accum[r],
+        // out_len[r] (a per-lane address, so hipcc makes no early scalar copy of them, whose wait
+        // would sit in front of the W_hidden loads)
+        const int32_t* bk = ln == 1   ? reinterpret_cast<const int32_t*>(gs.accum + r)
+                            : ln == 2 ? gs.out_len + r
+                                      : reinterpret_cast<const int32_t*>(gs.fin + (r & ~3));
+        bkv = *bk;
+      } else {
+        tq = cell.tok[r];
+      }
+      load_wh();
+      __builtin_amdgcn_sched_barrier(0);  // no use of the select's operands is hoisted above the W_hidden loads
       int dn_sel, dn;
-      done_before2(newdone, cell.gs.lsel, l, dn_sel, dn);
+      done_reduce(cnt, gs.lsel, l, dn_sel, dn);
       int t = 0;
       if (cell.sel) {
-        const GreedySel& gs = cell.gs;
-        float m = -INFINITY, se = 0.f;
-        int mi = 0x7fffffff;
-        if (ln < gs.nbp) {
-          m = gs.gp.mx[(size_t)r * GP_NB + ln];
-          se = gs.gp.se[(size_t)r * GP_NB + ln];
-          mi = gs.gp.ix[(size_t)r * GP_NB + ln];
-        }
-        load_wh();
-        uint8_t fin0 = 0;
-        float acc0 = 0.f;
-        int len0 = 0;
-        if (ln == 0) {
-          fin0 = gs.fin[r];
-          acc0 = gs.accum[r];
-          len0 = gs.out_len[r];
-        }
+        const bool in = ln < gs.nbp;
+        m = in ? m : -INFINITY;
+        se = in ? se : 0.f;
+        mi = in ? mi : 0x7fffffff;
         if (dn_sel < total) {  // else nothing downstream runs any more
           float gm = m;
           int gi = mi;
@@ -221,14 +234,16 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
           const bool bad_t = (unsigned)t >= (unsigned)V;  // no finite maximum (NaN row)
           if (bad_t) t = 0;
           const float sx = wave_sum((se > 0.f) ? se * expf(m - gm) : 0.f);
+          const uint8_t fin0 = (uint8_t)((uint32_t)__builtin_amdgcn_readlane(bkv, 0) >> (8 * (r & 3)));
+          const float acc0 = __int_as_float(__builtin_amdgcn_readlane(bkv, 1));
+          const int len0 = __builtin_amdgcn_readlane(bkv, 2);
           if (ln == 0) {
             if (bad_t) atomicOr(cell.err, CASR_DEV_NAN_LOGITS);
             greedy_book(gs, r, t, gm - (logf(sx) + gm), fin0, acc0, len0);
           }
         }
       } else {
-        t = cell.tok[r];
-        load_wh();
+        t = tq;
         if ((unsigned)t >= (unsigned)V) {
           if (ln == 0) atomicOr(cell.err, CASR_DEV_BAD_TOKEN);
           t = 0;
@@ -239,6 +254,9 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
         skip_s = dn >= total;
       }
       load_prev();
+    } else {  // (an else branch: wave 0's code is not joined behind these loads)
+      load_prev();
+      load_wh();
     }
     __syncthreads();
     stamp(6);  // (diagnostics) the select and its bookkeeping done

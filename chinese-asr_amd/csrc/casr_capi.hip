@@ -920,7 +920,9 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a, bool greedy) {
   // the folded greedy attention (attention_kernel<1, 1>) holds its cell-phase area on top of the
   // three-launch step's LDS: at Tp where only the latter fits, greedy keeps the three-launch step
   const bool fold_lds = !greedy || attention_smem_bytes(B, k, Tp, h->tune[CASR_OPT_ATTN_KPB], 1) <= 160 * 1024;
-  a.fold = (greedy || fold_beam) && fold_vocab && fold_lds && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
+  // the folded greedy attention reads the early-exit counters of steps 0..max_len-1 one per lane
+  const bool fold_len = !greedy || L <= 64;
+  a.fold = (greedy || fold_beam) && fold_vocab && fold_lds && fold_len && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
   if (a.fold) {
     HIP_OK(h, h->fgates.ensure((size_t)R * 4 * HD * sizeof(float)));
     a.fb = FoldBufs{h->wfold.as<float>(), h->egates.as<float>(), h->wq16.as<float>(), h->fgates.as<float>()};

@@ -183,6 +183,24 @@ CASR_DEV int done_before(const int32_t* __restrict__ newdone, int l) {
          (__builtin_amdgcn_readlane(s, 32) + __builtin_amdgcn_readlane(s, 48));
 }
 
+// done_before2 for at most 64 steps in two halves: the counters' load (lane i: step i) and its
+// reduction, so a caller can issue other loads in between without its wait for the counters waiting
+// for them too (a wave's loads retire in issue order)
+CASR_DEV int done_load(const int32_t* __restrict__ newdone, int lm) {
+  const int lane = threadIdx.x & 63;
+  return lane < lm ? newdone[lane] : 0;
+}
+CASR_DEV void done_reduce(int v, int l1, int l2, int& d1, int& d2) {
+  const int lane = threadIdx.x & 63;
+  int s1 = lane < l1 ? v : 0, s2 = lane < l2 ? v : 0;
+  s1 = row16_isum(s1);
+  s2 = row16_isum(s2);
+  d1 = (__builtin_amdgcn_readlane(s1, 0) + __builtin_amdgcn_readlane(s1, 16)) +
+       (__builtin_amdgcn_readlane(s1, 32) + __builtin_amdgcn_readlane(s1, 48));
+  d2 = (__builtin_amdgcn_readlane(s2, 0) + __builtin_amdgcn_readlane(s2, 16)) +
+       (__builtin_amdgcn_readlane(s2, 32) + __builtin_amdgcn_readlane(s2, 48));
+}
+
 // rows finished before steps l1 and l2 from one pass of loads over the counters
 CASR_DEV void done_before2(const int32_t* __restrict__ newdone, int l1, int l2, int& d1, int& d2) {
   const int lane = threadIdx.x & 63, lm = max(l1, l2);
