@@ -39,6 +39,7 @@ __host__ __device__ constexpr int attn_scratch_floats(int Tq) {
 // the folded step's cell phase (CELL): h [HD] | query slices [AT_QS][A]
 constexpr int AT_QS = AT_THREADS / (A / 4);  // 16 unit slices of HD / AT_QS = 32 units
 constexpr int AT_CELL_FLOATS = HD + AT_QS * A;
+static_assert(AT_QS * A >= 4 * HD, "the token's gate-table row fits the query slice area (CELL 1)");
 
 // LDS: qs, eqs [AT_APAD][KPB] | vs, v2s [A] | (AT_MAXG unused) | scratch | es [Tq][KPB] | (CELL: h,
 // query slices) | value rows
@@ -146,23 +147,39 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   // cell phase, which it does not depend on, so the scores start on landed keys
   constexpr bool PRE = CELL == 1 || (CELL == 2 && KPB >= 8);  // (KPB 4: 20 keys rows per batch, no registers left)
   float4 kvp[PRE ? CH : 1];
+  // CELL 1, 2 (round 4): unconditional loads at clamped addresses, masked at use.  Per-slot
+  // conditional loads compile to lane-masked regions, and their joins made hipcc wait for every load
+  // in flight (the preload now follows the gathers and W_hidden loads of the cell phase).  CELL 0
+  // keeps the conditional form
   auto preload_keys = [&]() {
     const int ag = tid / nch, t0 = 4 * (tid - ag * nch), a0 = ag * apg, a1 = min(A, a0 + apg);
     const bool live = !direct && tid < G * nch && t0 < len;
+    if constexpr (CELL != 0) {  // raw values: the slots past a1 / dead items are zeroed at use (score_item)
+      const int tc = min(t0, Tq - 4);
 #pragma unroll
-    for (int i = 0; i < CH; ++i)
-      kvp[i] = live && a0 + i < a1 ? *reinterpret_cast<const float4*>(ekb + (size_t)(a0 + i) * Tq + t0)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int i = 0; i < CH; ++i)
+        kvp[i] = *reinterpret_cast<const float4*>(ekb + (size_t)min(a0 + i, A - 1) * Tq + tc);
+      (void)live;
+      (void)a1;
+    } else {
+#pragma unroll
+      for (int i = 0; i < CH; ++i)
+        kvp[i] = live && a0 + i < a1 ? *reinterpret_cast<const float4*>(ekb + (size_t)(a0 + i) * Tq + t0)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
-  if constexpr (PRE && CELL != 1) preload_keys();
+  if constexpr (PRE && CELL == 0) preload_keys();
   if constexpr (CELL == 1) {
     // 0. the folded step's LSTM cell (decoder.py:104-114) and query (attention.py:92) for row r.
     // Load order (round 4): a wave's loads retire in issue order, so whatever a wave issues first is
-    // what it waits on first.  Wave 0 issues the select's partials before anything else (they were
-    // queued behind the block's whole keys batch, ~136 KB, before); the previous step's gate
-    // pre-activations of unit u = tid and its c and the W_hidden slice (rows 32 us .. +31, columns
-    // 4 a4 .. +3) follow; after the select, the token's gate-table row, then the first keys batch:
-    // the keys stream in under the cell and the query
+    // what it waits on first.  Waves 1..7 issue the previous step's gate pre-activations of unit
+    // u = tid and its c, their W_hidden slices (rows 32 us .. +31, columns 4 a4 .. +3) and their
+    // first keys batch at once, and wait at the barrier.  Wave 0 issues the select's operands
+    // first, selects the token, then gathers the token's gate-table row (8 KB) into LDS (the query
+    // slice area, free until the query) with nothing else of its own in flight, and only then
+    // issues its W_hidden slice and keys.  So the cell reads its gate row from LDS instead of each
+    // wave waiting for its own gather behind the keys stream (phase trace, profiles/r04: select
+    // 2.8 us, cell 5.2 us, query 0.8 us p50 with the gathers per wave)
     __shared__ int tk_s, skip_s;
     const int r = (int)row0;
     const int a4 = tid & (A / 4 - 1), us = tid / (A / 4);
@@ -216,8 +233,6 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       } else {
         tq = cell.tok[r];
       }
-      load_wh();
-      __builtin_amdgcn_sched_barrier(0);  // no use of the select's operands is hoisted above the W_hidden loads
       int dn_sel, dn;
       done_reduce(cnt, gs.lsel, l, dn_sel, dn);
       int t = 0;
@@ -253,19 +268,29 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
         tk_s = t;
         skip_s = dn >= total;
       }
+      // the token's gate-table row (4 HD floats, packed gate-row order) into LDS by LDS-DMA: 8 KB,
+      // no registers, and wave 0's only loads in flight (the select's operands have landed), so
+      // the wait for them is one gather round trip; then wave 0's own W_hidden and keys loads
+      {
+        const float* src = cell.emb_gates + (size_t)t * (4 * HD);
+#pragma unroll
+        for (int i = 0; i < 4 * HD / 256; ++i) lds_dma16(src + 256 * i + 4 * ln, hs + HD + 256 * i);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      load_wh();
       load_prev();
+      preload_keys();
     } else {  // (an else branch: wave 0's code is not joined behind these loads)
       load_prev();
       load_wh();
+      preload_keys();
     }
     __syncthreads();
-    stamp(6);  // (diagnostics) the select and its bookkeeping done
+    stamp(6);  // (diagnostics) the select, its bookkeeping and the gate-row gather done
     if (skip_s) return;
-    const int t = tk_s;
     float eg[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) eg[g] = cell.emb_gates[(size_t)t * (4 * HD) + gcol(g, u)];
-    preload_keys();
+    for (int g = 0; g < 4; ++g) eg[g] = hs[HD + gcol(g, u)];
     float h2, c2;
     lstm_cell_hw(gprev[0] + eg[0], gprev[1] + eg[1], gprev[2] + eg[2], gprev[3] + eg[3], cold, h2, c2);
     st[(size_t)r * ST + C + u] = h2;
@@ -337,6 +362,10 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
         bl[ks] = *reinterpret_cast<const f16x8*>(fb + 256);
       }
     }
+    // (round 4) the first keys batch after the gathers and the W_hidden fragments: a wave's loads
+    // retire in issue order, so the cells' wait for their gathers no longer covers the block's whole
+    // keys batch (the beam prologue took 13.3 us p50 with the keys issued first, profiles/r04)
+    if constexpr (PRE) preload_keys();
 #pragma unroll
     for (int j = 0; j < KPB; ++j) {
       float h2 = 0.f, c2;
@@ -489,7 +518,8 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       float4 kv[CH];
       if constexpr (PRE && split) {  // preloaded before the cell phase (it == tid)
 #pragma unroll
-        for (int i = 0; i < CH; ++i) kv[i] = kvp[i];
+        for (int i = 0; i < CH; ++i)
+          kv[i] = CELL == 0 || (live && ab + i < a1) ? kvp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         load(kv, ab);
       }

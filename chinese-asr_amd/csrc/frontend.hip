@@ -74,6 +74,10 @@ CASR_DEV void lds_fence() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// FPW frames per wave.  A lane's mel-filter weights (filters lane and lane + 64) are read from LDS
+// once into registers for all its frames: 7 % faster than an LDS read per weight and frame at the
+// same bits (tools/probes/logmel_variants.hip, profiles/r04/logmel/variants_r04g.txt)
+template <int FPW = FE_FPW>
 __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ wav,
                                                       const int32_t* __restrict__ nsamp, int Nmax,
                                                       int Tmax, float pre, const FrontendConst* __restrict__ k,
@@ -101,7 +105,7 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
   }
   const int L = n - 1 >= NFFT ? 1 + (n - 1 - NFFT) / HOP : 0;  // frames of the pre-emphasised signal
   if (blockIdx.x == 0 && threadIdx.x == 0) frames[b] = L < Tmax ? L : Tmax;
-  const int f0 = (blockIdx.x * FE_WAVES + w) * FE_FPW;
+  const int f0 = (blockIdx.x * FE_WAVES + w) * FPW;
   if (f0 >= Tmax) return;  // no block barrier below: the waves are independent
   // per-lane constants of every frame: window values of the lane's 8 samples, the twiddles of the
   // three twiddled stages (group offset j of the lane: lane, lane & 15, lane & 3), the split twiddles
@@ -134,7 +138,13 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
     }
   };
   load_frame(f0);
-  for (int fi = 0; fi < FE_FPW; ++fi) {
+  // this lane's weights of filters lane (pass 0) and lane + 64 (pass 1)
+  float fw0[FE_W0], fw1[FE_W1];
+#pragma unroll
+  for (int i = 0; i < FE_W0; ++i) fw0[i] = fbs[lane][i];
+#pragma unroll
+  for (int i = 0; i < FE_W1; ++i) fw1[i] = lane + 64 < F ? fbs[lane + 64][i] : 0.f;
+  for (int fi = 0; fi < FPW; ++fi) {
     const int f = f0 + fi;
     if (f >= Tmax) break;
     float* o = out + ((size_t)b * Tmax + f) * F;
@@ -147,7 +157,7 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       a[r] = make_float2(preemph_win(wn[r][0], xs[r][1], xs[r][0], pre), preemph_win(wn[r][1], xs[r][2], xs[r][1], pre));
-    if (fi + 1 < FE_FPW) load_frame(f + 1);
+    if (fi + 1 < FPW) load_frame(f + 1);
     // stage 0 (S = 64): the lane's points are its butterfly
     float2 tw[3];
     twiddles(0, tw);
@@ -203,22 +213,22 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
     // 0..63 (at most FE_W0 bins), pass 1 = filters 64..79 on lanes 0..15 (at most FE_W1 bins).  The
     // weights past a filter's last bin are zero (fma(x, 0, acc) = acc for the finite powers; a
     // non-finite power makes the sum NaN, as the reference's full-length matmul does)
-    auto mel = [&](auto NW, int m) {
+    auto mel = [&](auto NW, int m, const float* wreg) {  // (the weights from registers, in bin order)
       constexpr int W = decltype(NW)::value;
       const int lo = lohi[0][m];
       float pv[W], wv[W];
 #pragma unroll
       for (int i = 0; i < W; ++i) {
         pv[i] = pw[w][min(lo + i, NBIN - 1)];
-        wv[i] = fbs[m][i];
+        wv[i] = wreg[i];
       }
       float acc = 0.f;
 #pragma unroll
       for (int i = 0; i < W; ++i) acc = fmaf(pv[i], wv[i], acc);  // matmul: fused
       o[m] = logf(acc == 0.f ? 1.1920928955078125e-07f : acc);
     };
-    mel(std::integral_constant<int, FE_W0>{}, lane);
-    if (lane + 64 < F) mel(std::integral_constant<int, FE_W1>{}, lane + 64);
+    mel(std::integral_constant<int, FE_W0>{}, lane, fw0);
+    if (lane + 64 < F) mel(std::integral_constant<int, FE_W1>{}, lane + 64, fw1);
     lds_fence();  // this frame's pw / zs reads are done before the next frame's writes
   }
 }
@@ -290,7 +300,7 @@ hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nma
                           const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s) {
   constexpr int FPB = FE_WAVES * FE_FPW;  // frames per block
   dim3 grid((Tmax + FPB - 1) / FPB > 0 ? (Tmax + FPB - 1) / FPB : 1, B);
-  hipLaunchKernelGGL(log_mel_kernel, grid, dim3(256), 0, s, wav, nsamp, Nmax, Tmax, pre, k, out, frames, err);
+  hipLaunchKernelGGL(log_mel_kernel<>, grid, dim3(256), 0, s, wav, nsamp, Nmax, Tmax, pre, k, out, frames, err);
   return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@ from casr.weights import synthetic_state_dicts  # noqa: E402
 B, T = int(os.environ.get("B", 256)), 800
 
 
-def attn_report(r, title):
+def attn_report(r, title, sub=True):
     r = r[r[:, 0] > 0]
     t = (r[:, :6] - r[:, 0].min()) * 10 / 1000.0
     print(f"{title}: {len(r)} blocks, span {t[:, 5].max():.2f} us")
@@ -29,7 +29,7 @@ def attn_report(r, title):
         print(f"  {n:14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
     v = t[:, 0]
     print(f"  {'start':14s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  p90 {np.percentile(v, 90):6.2f}")
-    if (r[:, 6] > 0).all() and (r[:, 7] > 0).all():  # the folded step's prologue (CELL 1 stamps 6, 7)
+    if sub and (r[:, 6] > 0).all() and (r[:, 7] > 0).all():  # the folded greedy prologue (CELL 1 stamps 6, 7)
         t6 = (r[:, 6] - r[:, 0].min()) * 10 / 1000.0
         t7 = (r[:, 7] - r[:, 0].min()) * 10 / 1000.0
         for n, v in (("  select", t6 - t[:, 0]), ("  cell", t7 - t6), ("  query", t[:, 1] - t7)):
@@ -66,7 +66,7 @@ if os.environ.get("BEAM"):
     r = raw[2]
     r = r[r[:, 0] > 0]
     t = (r[:, :7] - r[:, 0].min()) * 10 / 1000.0
-    attn_report(raw[3], "attention (beam)")
+    attn_report(raw[3], "attention (beam)", sub=False)
     gemm_report(raw, "beam")
     names = ["lse+partials", "tau+offer", "list insert", "row merge", "block merge", "bookkeeping"]
     print(f"beam_select: {len(r)} blocks, span {t[:, 6].max():.2f} us, candidates (wave 0) p50 {np.median(r[:, 7]):.0f} max {r[:, 7].max()}")
