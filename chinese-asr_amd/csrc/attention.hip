@@ -19,6 +19,12 @@
 #include "casr_common.h"
 #include "casr_internal.h"
 
+// (diagnostic builds only, tools/probes: bit 0 drops the greedy prologue's W_hidden loads, bit 1
+// its gate-row gather; the results are then wrong)
+#ifndef CASR_AT_DIAG
+#define CASR_AT_DIAG 0
+#endif
+
 namespace casr {
 
 constexpr int AT_THREADS = 512;
@@ -201,7 +207,8 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     auto load_wh = [&]() {
 #pragma unroll
       for (int i = 0; i < UPS; ++i)
-        wh[i] = *reinterpret_cast<const float4*>(cell.w_hidden + (size_t)(UPS * us + i) * A + 4 * a4);
+        wh[i] = (CASR_AT_DIAG & 1) ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                   : *reinterpret_cast<const float4*>(cell.w_hidden + (size_t)(UPS * us + i) * A + 4 * a4);
     };
     if (wv == 0) {  // the select of step l - 1 (greedy_select_part_kernel's arithmetic) and its bookkeeping
       // rows finished before step l - 1 (the select's own skip) and before step l (the block's early
@@ -274,7 +281,8 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       {
         const float* src = cell.emb_gates + (size_t)t * (4 * HD);
 #pragma unroll
-        for (int i = 0; i < 4 * HD / 256; ++i) lds_dma16(src + 256 * i + 4 * ln, hs + HD + 256 * i);
+        for (int i = 0; i < 4 * HD / 256; ++i)
+          if (!(CASR_AT_DIAG & 2)) lds_dma16(src + 256 * i + 4 * ln, hs + HD + 256 * i);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       load_wh();

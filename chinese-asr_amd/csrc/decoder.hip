@@ -178,6 +178,11 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
     if (dtr && tid == 0) dtr[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
+  if (dtr && tid == 0) {  // the block's tile (words 5, 6) and the launch's column block count (7)
+    dtr[5] = (uint32_t)nb;
+    dtr[6] = (uint32_t)rb;
+    dtr[7] = (uint32_t)NB;
+  }
   const int r = lane & 15, g = lane >> 4;
   const int cnt_w = w < NDMA ? (NDMA - w + 7) / 8 : 0;  // DMA instructions this wave issues per stage
 
@@ -725,7 +730,10 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
 // segments (one instruction covers 64 consecutive float4 of the tile, row-major: up to 640
 // contiguous bytes per row), and each 16-column tile's maximum (tmx, for the beam select's
 // threshold and candidate tiles; tiles < ntl only) is reduced over the quad of lanes that hold it.
-template <int NTN>
+// FULL: every column of the block is a vocabulary column < V, no gate column, and V % 4 == 0 (the
+// common block): no per-element column tests.  The tile maxima of a wave are stored together after
+// its segments (one masked region instead of one per segment).  Same values either way.
+template <int NTN, bool FULL = false>
 __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const float (&bn)[16], int row0, int nb,
                                                 int u, float* scr, float* logits, float* tmx, int R, int V,
                                                 int ntl, float* gates = nullptr, int gcol0 = 0) {
@@ -739,19 +747,21 @@ __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const f
   __builtin_amdgcn_wave_barrier();
   const int rb0 = row0 - 4 * g, c0 = nb * 16 * NTN;
   const bool vec = (V & 3) == 0;
+  float tm[CH / 4];
 #pragma unroll
   for (int i = 0; i < CH / 4; ++i) {
     const int f = i * 64 + lane, rr = f / CH, ch = f - rr * CH;
     const float4 v = *reinterpret_cast<const float4*>(scr + rr * RWS + 4 * ch);
     const int row = rb0 + rr, col = c0 + 4 * ch;
-    if (gates && col >= gcol0) {  // (FoldEpi) the next step's gate pre-activations: raw, no bias
+    tm[i] = -INFINITY;
+    if (!FULL && gates && col >= gcol0) {  // (FoldEpi) the next step's gate pre-activations: raw, no bias
       if (row < R && col - gcol0 < 4 * HD) *reinterpret_cast<float4*>(gates + (size_t)row * (4 * HD) + (col - gcol0)) = v;
       continue;
     }
-    if (!logits) continue;
-    if (row < R) {
+    if (!logits && !tmx) continue;
+    if (logits && row < R) {
       float* dst = logits + (size_t)row * V + col;
-      if (vec && col + 3 < V) {
+      if (FULL || (vec && col + 3 < V)) {
         *reinterpret_cast<float4*>(dst) = v;
       } else {
         if (col < V) dst[0] = v.x;
@@ -761,51 +771,93 @@ __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const f
       }
     }
     if (tmx) {
-      float m = fmaxf(fmaxf(col < V ? v.x : -INFINITY, col + 1 < V ? v.y : -INFINITY),
-                      fmaxf(col + 2 < V ? v.z : -INFINITY, col + 3 < V ? v.w : -INFINITY));
+      float m = FULL ? fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w))
+                     : fmaxf(fmaxf(col < V ? v.x : -INFINITY, col + 1 < V ? v.y : -INFINITY),
+                             fmaxf(col + 2 < V ? v.z : -INFINITY, col + 3 < V ? v.w : -INFINITY));
       m = fmaxf(m, dpp_f<DPP_XOR1>(m));
-      m = fmaxf(m, dpp_f<DPP_XOR2>(m));
-      if ((lane & 3) == 0 && row < R && (col >> 4) < ntl) tmx[(size_t)row * GP_NT + (col >> 4)] = m;
+      tm[i] = fmaxf(m, dpp_f<DPP_XOR2>(m));
+    }
+  }
+  if (tmx && (lane & 3) == 0) {
+#pragma unroll
+    for (int i = 0; i < CH / 4; ++i) {
+      const int f = i * 64 + lane, rr = f / CH, ch = f - rr * CH;
+      const int row = rb0 + rr, col = c0 + 4 * ch;
+      if (row < R && (col >> 4) < ntl && (FULL || !gates || col < gcol0)) tmx[(size_t)row * GP_NT + (col >> 4)] = tm[i];
     }
   }
 }
 
 // per-row partials over the block's columns n < V (greedy, and beam at temperature 1): lane (g, u)
-// holds columns 16 (nb NTN + tn) + u; the 16 lanes of one g share the rows
-template <int NTN>
+// holds columns 16 (nb NTN + tn) + u; the 16 lanes of one g share the rows.  The four rows' shuffle
+// trees run side by side and the partials are stored together at the end (FULL: no column tests).
+template <int NTN, bool FULL = false>
 __device__ __forceinline__ void proj_row_partials(const f32x4 (&acc)[NTN], const float (&bn)[16], int row0, int nb,
                                                   int u, const GreedyPart& gp, int R, int V) {
+  float x[4][NTN], m[4], sx[4];
+  int mi[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    float x[NTN];
-    float m = -INFINITY;
-    int mi = 0x7fffffff;
+    m[e] = -INFINITY;
+    mi[e] = 0x7fffffff;
 #pragma unroll
     for (int tn = 0; tn < NTN; ++tn) {
       const int n = (nb * NTN + tn) * 16 + u;
-      x[tn] = acc[tn][e] + bn[tn];
-      if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
-        m = x[tn];
-        mi = n;
+      x[e][tn] = acc[tn][e] + bn[tn];
+      if ((FULL || n < V) && x[e][tn] > m[e]) {  // columns ascend with tn: first index within the lane
+        m[e] = x[e][tn];
+        mi[e] = n;
       }
     }
-    {  // the row's (max, lowest column among equal maxima) over the 16 lanes of this g
-      const float rm = row16_max(m);
-      mi = row16_min(m == rm ? mi : 0x7fffffff);
-      m = rm;
-    }
-    float sx = 0.f;
+  }
+  // the rows' (max, lowest column among equal maxima) over the 16 lanes of this g
+  float rm[4];
+  int ri[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) rm[e] = fmaxf(m[e], dpp_f<DPP_XOR1>(m[e]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) rm[e] = fmaxf(rm[e], dpp_f<DPP_XOR2>(rm[e]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) rm[e] = fmaxf(rm[e], dpp_f<DPP_ROR4>(rm[e]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) rm[e] = fmaxf(rm[e], dpp_f<DPP_ROR8>(rm[e]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ri[e] = m[e] == rm[e] ? mi[e] : 0x7fffffff;
+    ri[e] = min(ri[e], dpp_i<DPP_XOR1>(ri[e]));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) ri[e] = min(ri[e], dpp_i<DPP_XOR2>(ri[e]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) ri[e] = min(ri[e], dpp_i<DPP_ROR4>(ri[e]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) ri[e] = min(ri[e], dpp_i<DPP_ROR8>(ri[e]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sx[e] = 0.f;
 #pragma unroll
     for (int tn = 0; tn < NTN; ++tn) {
       const int n = (nb * NTN + tn) * 16 + u;
-      if (n < V) sx += expf(x[tn] - m);
+      if (FULL || n < V) sx[e] += expf(x[e][tn] - rm[e]);
     }
-    sx = row16_sum(sx);  // lane u == 0 (the row's first quad) writes it
-    const int row = row0 + e;
-    if (u == 0 && row < R) {
-      gp.mx[(size_t)row * GP_NB + nb] = m;
-      gp.se[(size_t)row * GP_NB + nb] = sx;
-      gp.ix[(size_t)row * GP_NB + nb] = mi;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sx[e] += dpp_f<DPP_XOR1>(sx[e]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sx[e] += dpp_f<DPP_XOR2>(sx[e]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sx[e] += dpp_f<DPP_ROR4>(sx[e]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) sx[e] += dpp_f<DPP_ROR8>(sx[e]);
+  if (u == 0) {  // lane u == 0 (the rows' first quad) writes them
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = row0 + e;
+      if (row < R) {
+        gp.mx[(size_t)row * GP_NB + nb] = rm[e];
+        gp.se[(size_t)row * GP_NB + nb] = sx[e];
+        gp.ix[(size_t)row * GP_NB + nb] = ri[e];
+      }
     }
   }
 }
@@ -886,11 +938,21 @@ struct FoldEpi {
     // gate columns of consecutive tiles are consecutive in gates[row]; VT 16 is a multiple of 4, so
     // no segment straddles the two); the biases of the gate tiles are 0 (Pre), the stored values raw
     const bool has_gates = (nb + 1) * NTN > VT;
-    if (logits || has_gates)
-      proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, VT, has_gates ? gates : nullptr,
-                           16 * VT);
+    // a block of vocabulary columns only, all < V (every block but the last vocabulary one)
+    const bool full = (nb + 1) * NTN * 16 <= V && (V & 3) == 0;
+    // (CASR_DG_DIAG ablation builds only: bit 5 drops the logits stores, bit 6 the tile maxima,
+    // bit 4 the row partials)
+    float* lg = (CASR_DG_DIAG & 32) ? nullptr : logits;
+    float* tm = (CASR_DG_DIAG & 64) ? nullptr : gp.tmx;
+    if (full) {
+      if (lg || tm) proj_logits_out<NTN, true>(acc, p.bn, row0, nb, u, scr, lg, tm, R, V, VT);
+      if (gp.mx && !(CASR_DG_DIAG & 16)) proj_row_partials<NTN, true>(acc, p.bn, row0, nb, u, gp, R, V);
+      return;
+    }
+    if (lg || tm || has_gates)
+      proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, lg, tm, R, V, VT, has_gates ? gates : nullptr, 16 * VT);
     if (nb * NTN >= VT) return;  // no vocabulary tile in this block
-    if (gp.mx) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
+    if (gp.mx && !(CASR_DG_DIAG & 16)) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
   }
 };
 
@@ -1878,6 +1940,19 @@ static uint32_t* dg_trace_buffer() {
 
 void dg_trace_init() { dg_trace_buffer(); }
 
+// CASR_DG_TRACE_STEP=<l> (diagnostics): the fused decode GEMM records its stamps at step l only
+// (before: every launch, the last one's surviving)
+static void dg_trace_step_gate(int l, bool before, hipStream_t s) {
+  static const int step = std::getenv("CASR_DG_TRACE_STEP") ? std::atoi(std::getenv("CASR_DG_TRACE_STEP")) : -1;
+  uint32_t* buf = dg_trace_buffer();
+  if (!buf || step < 0) return;
+  static uint32_t* on = nullptr;
+  static uint32_t* const off = nullptr;
+  on = buf;
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dg_trace), (before && l != step) ? &off : &on, sizeof(on), 0,
+                               hipMemcpyHostToDevice, s);
+}
+
 void dg_trace_dump() {
   uint32_t* buf = dg_trace_buffer();
   const char* path = std::getenv("CASR_DG_TRACE");
@@ -1906,7 +1981,9 @@ static void fold_gemm_step(const DecodeArgs& a, DecodeBufs& d, int l, int total,
   GreedyPart gp = row_partials(a) ? d.part : GreedyPart{nullptr, nullptr, nullptr, nullptr};
   if (!beam || a.V > 16 * GP_NT) gp.tmx = nullptr;  // tile maxima: beam only
   FoldEpi epi{a.W + a.L.proj_b, d.newdone, R, a.V, VT, l, total, d.err, gp, a.fb.gates, beam ? d.logits : nullptr};
+  dg_trace_step_gate(l, true, s);
   launch_fold_gemm(R, beam, NB, ntiles, a.fb.wfold, asrc, epi, s);
+  dg_trace_step_gate(l, false, s);
 }
 
 // the folded step's attention with its cell prologue (steps l >= 1): greedy with the fused select

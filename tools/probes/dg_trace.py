@@ -37,7 +37,8 @@ def attn_report(r, title, sub=True):
 def gemm_report(raw, tag):
     for cls, name in ((0, "dec_lstm"), (1, "proj")):
         r = raw[cls]
-        r = r[r[:, 0] > 0]
+        bid = np.nonzero(r[:, 0] > 0)[0]  # blockIdx.x of the stamped blocks
+        r = r[bid]
         t = (r[:, :5] - r[:, 0].min()) * 10 / 1000.0  # us
         span = t[:, 4].max()
         ph = {"start": t[:, 0], "prologue": t[:, 1] - t[:, 0], "first tile": t[:, 2] - t[:, 1],
@@ -46,6 +47,20 @@ def gemm_report(raw, tag):
         for k, v in ph.items():
             print(f"  {k:12s} p10 {np.percentile(v, 10):6.2f}  p50 {np.percentile(v, 50):6.2f}  "
                   f"p90 {np.percentile(v, 90):6.2f}  max {v.max():6.2f}")
+        if os.environ.get("CASR_DG_TRACE_STEP") and cls == 1 and (r[:, 7] > 0).all():
+            # one step's fused GEMM: blocks by column-block kind (words 5-7: nb, rb, NB) and by XCD
+            nb, nt = r[:, 5], int(os.environ.get("NTN", 14))
+            V = 5004
+            kind = np.where((nb + 1) * nt * 16 <= V, 0, np.where(nb * nt * 16 < V, 1, 2))
+            xcd = bid % 8
+            for kk, kn in enumerate(("vocabulary", "boundary", "gates")):
+                m = kind == kk
+                if m.any():
+                    print(f"    {kn:10s} {m.sum():3d} blocks: k loop p50 {np.median(ph['k loop'][m]):6.2f} max "
+                          f"{ph['k loop'][m].max():6.2f}  epilogue p50 {np.median(ph['epilogue'][m]):6.2f} max "
+                          f"{ph['epilogue'][m].max():6.2f}  end p50 {np.median(t[m, 4]):6.2f} max {t[m, 4].max():6.2f}")
+            ends = " ".join(f"{t[xcd == x, 4].max():6.2f}" for x in range(8) if (xcd == x).any())
+            print(f"    end max per blockIdx % 8: {ends}")
 
 
 cfg = CasrConfig()

@@ -29,12 +29,18 @@ using namespace casr;
     }                                                                              \
   } while (0)
 
-template <int FPW>
+#ifdef FE_NI  // a kernel source with the frames-in-flight parameter (log_mel_kernel<FPW, NI>)
+#define FE_KERNEL(FPW, NI) log_mel_kernel<FPW, NI>
+#else
+#define FE_KERNEL(FPW, NI) log_mel_kernel<FPW>
+#endif
+
+template <int FPW, int NI = 1>
 static float run(const char* name, const float* wav, const int* ns, int B, int N, int T, const FrontendConst* k,
                  float* out, int* fr, int* err, const std::vector<float>* ref, std::vector<float>* keep) {
   constexpr int FPB = 4 * FPW;
   dim3 grid((T + FPB - 1) / FPB, B);
-  auto go = [&] { hipLaunchKernelGGL((log_mel_kernel<FPW>), grid, dim3(256), 0, nullptr, wav, ns, N, T, 0.97f, k, out, fr, err); };
+  auto go = [&] { hipLaunchKernelGGL((FE_KERNEL(FPW, NI)), grid, dim3(256), 0, nullptr, wav, ns, N, T, 0.97f, k, out, fr, err); };
   go();
   (void)hipDeviceSynchronize();
   hipEvent_t e0, e1;
@@ -94,6 +100,12 @@ int main() {
   run<8>("v0 FPW 8 (default)", wav, nsd, B, N, T, k, out, fr, err, nullptr, &ref);
   run<4>("v1 FPW 4", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
   run<16>("v2 FPW 16", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+#ifdef FE_NI
+  run<8, 2>("v3 FPW 8, 2 frames in flight", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+  run<16, 2>("v4 FPW 16, 2 frames in flight", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+  run<8, 4>("v5 FPW 8, 4 frames in flight", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+  run<8, 1>("v6 FPW 8 (NI template, 1)", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+#endif
   int he = 0;
   (void)hipMemcpy(&he, err, 4, hipMemcpyDeviceToHost);
   std::printf("device flags %d\n", he);
