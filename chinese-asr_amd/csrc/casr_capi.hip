@@ -179,6 +179,9 @@ struct casr_handle {
   // per-token gate table, built at bind from an s16-valid blob; the gates buffer [R][4 HD]
   DevBuf wfold, egates, fgates, wq16;
   bool fold_ready = false;
+  // (round 4) the f32 fused image: the folded greedy step under the exact-f32 arithmetic
+  DevBuf wfold32;
+  bool fold32_ready = false;
   bool s16() const { return precision == CASR_PREC_S16X3 && s16_valid; }
   int B = 0, Tp = 0;
   bool encoded = false;
@@ -459,15 +462,21 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
   h->graphs.clear();  // captured graphs bake in the precision and weight pointers
   // the folded greedy step's tables (decoder.hip build_fold): derived from this blob, so rebuilt
   // at every bind; a blob without valid s16 images keeps the three-launch step
-  h->fold_ready = false;
-  if (h->s16_valid) {
+  h->fold_ready = h->fold32_ready = false;
+  {
     const int V = h->cfg.vocab;
-    HIP_OK(h, h->wfold.ensure((size_t)(fold_vtiles(V) + FOLD_GT) * (KPROJ / 64) * FRAG * sizeof(float)));
+    const size_t img = (size_t)(fold_vtiles(V) + FOLD_GT) * (KPROJ / 64) * FRAG * sizeof(float);
+    HIP_OK(h, h->wfold32.ensure(img));
     HIP_OK(h, h->egates.ensure((size_t)V * 4 * HD * sizeof(float)));
-    HIP_OK(h, h->wq16.ensure(FOLD_WQ16_FLOATS * sizeof(float)));
-    HIP_OK(h, build_fold(h->W, h->L, V, h->wfold.as<float>(), h->egates.as<float>(), h->wq16.as<float>(), nullptr));
+    if (h->s16_valid) {
+      HIP_OK(h, h->wfold.ensure(img));
+      HIP_OK(h, h->wq16.ensure(FOLD_WQ16_FLOATS * sizeof(float)));
+    }
+    HIP_OK(h, build_fold(h->W, h->L, V, h->s16_valid ? h->wfold.as<float>() : nullptr, h->egates.as<float>(),
+                         h->s16_valid ? h->wq16.as<float>() : nullptr, h->wfold32.as<float>(), nullptr));
     HIP_OK(h, hipStreamSynchronize(nullptr));
-    h->fold_ready = true;
+    h->fold_ready = h->s16_valid;
+    h->fold32_ready = true;
   }
   return CASR_OK;
 }
@@ -500,7 +509,7 @@ void casr_destroy(casr_handle* h) {
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->gflags, &h->fe_const,
-                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout, &h->wfold,
+                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout, &h->wfold, &h->wfold32,
                     &h->egates, &h->fgates, &h->wq16})
     b->release();
   delete h;
@@ -922,10 +931,14 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a, bool greedy) {
   const bool fold_lds = !greedy || attention_smem_bytes(B, k, Tp, h->tune[CASR_OPT_ATTN_KPB], 1) <= 160 * 1024;
   // the folded greedy attention reads the early-exit counters of steps 0..max_len-1 one per lane
   const bool fold_len = !greedy || L <= 64;
-  a.fold = (greedy || fold_beam) && fold_vocab && fold_lds && fold_len && a.s16 && h->fold_ready && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
+  // greedy folds in either arithmetic (round 4: the exact-f32 MFMAs on the f32 fused image); the
+  // beam fold's one-accumulator shapes and its s16 query need the s16 images
+  const bool fold_arith = a.s16 ? h->fold_ready : (greedy && h->fold32_ready);
+  a.fold = (greedy || fold_beam) && fold_vocab && fold_lds && fold_len && fold_arith && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
   if (a.fold) {
     HIP_OK(h, h->fgates.ensure((size_t)R * 4 * HD * sizeof(float)));
-    a.fb = FoldBufs{h->wfold.as<float>(), h->egates.as<float>(), h->wq16.as<float>(), h->fgates.as<float>()};
+    a.fb = FoldBufs{a.s16 ? h->wfold.as<float>() : h->wfold32.as<float>(), h->egates.as<float>(), h->wq16.as<float>(),
+                    h->fgates.as<float>()};
   }
   return CASR_OK;
 }
@@ -954,7 +967,7 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   float* ial = align ? iacc + B : nullptr;
   uint8_t* ifin = reinterpret_cast<uint8_t*>(iacc + B + nal);
   a.prof = nullptr;
-  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)a.fold, (uint64_t)h->fgates.p, (uint64_t)h->wfold.p, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
+  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)a.fold, (uint64_t)h->fgates.p, (uint64_t)a.fb.wfold, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
                                      (uint64_t)(align != nullptr), (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->enc_out, (uint64_t)h->keysT.p,
                                      (uint64_t)h->hfin.p, (uint64_t)h->cst.p, (uint64_t)h->lens.p};

@@ -313,14 +313,17 @@ constexpr int FOLD_NT = 7;            // 16-column tiles per fused GEMM block (1
 inline int fold_vtiles(int V) { return (V + 15) / 16; }
 constexpr size_t FOLD_WQ16_FLOATS = (size_t)A * HD;  // the W_hidden fragment image (beam query)
 struct FoldBufs {
-  const float* wfold;      // s16 fragment image: [fold_vtiles(V) + FOLD_GT tiles][KPROJ / 64] FRAG blocks
+  const float* wfold;      // fragment image (s16, or f32 under the exact-f32 arithmetic):
+                           // [fold_vtiles(V) + FOLD_GT tiles][KPROJ / 64] FRAG blocks
   const float* emb_gates;  // [V][4 HD] packed gate-row order (packed_gate_row), biases included
   const float* wq16;       // s16 fragment image of W_hidden^T: [A / 16 tiles][HD / 64] FRAG blocks
   float* gates;            // [R][4 HD] the next step's [ctx | h] . W_ch^T, packed gate-row order
 };
-// build the fused image and the per-token gate table from a bound s16-valid blob (bind time)
+// build the fused images and the per-token gate table from a bound blob (bind time): wfold and
+// wq16 from the s16 images (nullptr: skipped, a blob without valid s16 images), wfold32 from the f32
+// fragment images (the folded greedy step under the exact-f32 arithmetic), emb_gates always
 hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, float* wq16,
-                      hipStream_t s);
+                      float* wfold32, hipStream_t s);
 
 struct DecodeBufs {
   float* st[2];          // [R][ST]

@@ -730,10 +730,7 @@ struct ProjA {  // A rows of the projection: st_new[r][0:1024] = [ctx | h] (s16:
 // segments (one instruction covers 64 consecutive float4 of the tile, row-major: up to 640
 // contiguous bytes per row), and each 16-column tile's maximum (tmx, for the beam select's
 // threshold and candidate tiles; tiles < ntl only) is reduced over the quad of lanes that hold it.
-// FULL: every column of the block is a vocabulary column < V, no gate column, and V % 4 == 0 (the
-// common block): no per-element column tests.  The tile maxima of a wave are stored together after
-// its segments (one masked region instead of one per segment).  Same values either way.
-template <int NTN, bool FULL = false>
+template <int NTN>
 __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const float (&bn)[16], int row0, int nb,
                                                 int u, float* scr, float* logits, float* tmx, int R, int V,
                                                 int ntl, float* gates = nullptr, int gcol0 = 0) {
@@ -747,21 +744,19 @@ __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const f
   __builtin_amdgcn_wave_barrier();
   const int rb0 = row0 - 4 * g, c0 = nb * 16 * NTN;
   const bool vec = (V & 3) == 0;
-  float tm[CH / 4];
 #pragma unroll
   for (int i = 0; i < CH / 4; ++i) {
     const int f = i * 64 + lane, rr = f / CH, ch = f - rr * CH;
     const float4 v = *reinterpret_cast<const float4*>(scr + rr * RWS + 4 * ch);
     const int row = rb0 + rr, col = c0 + 4 * ch;
-    tm[i] = -INFINITY;
-    if (!FULL && gates && col >= gcol0) {  // (FoldEpi) the next step's gate pre-activations: raw, no bias
+    if (gates && col >= gcol0) {  // (FoldEpi) the next step's gate pre-activations: raw, no bias
       if (row < R && col - gcol0 < 4 * HD) *reinterpret_cast<float4*>(gates + (size_t)row * (4 * HD) + (col - gcol0)) = v;
       continue;
     }
-    if (!logits && !tmx) continue;
-    if (logits && row < R) {
+    if (!logits) continue;
+    if (row < R) {
       float* dst = logits + (size_t)row * V + col;
-      if (FULL || (vec && col + 3 < V)) {
+      if (vec && col + 3 < V) {
         *reinterpret_cast<float4*>(dst) = v;
       } else {
         if (col < V) dst[0] = v.x;
@@ -771,93 +766,51 @@ __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const f
       }
     }
     if (tmx) {
-      float m = FULL ? fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w))
-                     : fmaxf(fmaxf(col < V ? v.x : -INFINITY, col + 1 < V ? v.y : -INFINITY),
-                             fmaxf(col + 2 < V ? v.z : -INFINITY, col + 3 < V ? v.w : -INFINITY));
+      float m = fmaxf(fmaxf(col < V ? v.x : -INFINITY, col + 1 < V ? v.y : -INFINITY),
+                      fmaxf(col + 2 < V ? v.z : -INFINITY, col + 3 < V ? v.w : -INFINITY));
       m = fmaxf(m, dpp_f<DPP_XOR1>(m));
-      tm[i] = fmaxf(m, dpp_f<DPP_XOR2>(m));
-    }
-  }
-  if (tmx && (lane & 3) == 0) {
-#pragma unroll
-    for (int i = 0; i < CH / 4; ++i) {
-      const int f = i * 64 + lane, rr = f / CH, ch = f - rr * CH;
-      const int row = rb0 + rr, col = c0 + 4 * ch;
-      if (row < R && (col >> 4) < ntl && (FULL || !gates || col < gcol0)) tmx[(size_t)row * GP_NT + (col >> 4)] = tm[i];
+      m = fmaxf(m, dpp_f<DPP_XOR2>(m));
+      if ((lane & 3) == 0 && row < R && (col >> 4) < ntl) tmx[(size_t)row * GP_NT + (col >> 4)] = m;
     }
   }
 }
 
 // per-row partials over the block's columns n < V (greedy, and beam at temperature 1): lane (g, u)
-// holds columns 16 (nb NTN + tn) + u; the 16 lanes of one g share the rows.  The four rows' shuffle
-// trees run side by side and the partials are stored together at the end (FULL: no column tests).
-template <int NTN, bool FULL = false>
+// holds columns 16 (nb NTN + tn) + u; the 16 lanes of one g share the rows
+template <int NTN>
 __device__ __forceinline__ void proj_row_partials(const f32x4 (&acc)[NTN], const float (&bn)[16], int row0, int nb,
                                                   int u, const GreedyPart& gp, int R, int V) {
-  float x[4][NTN], m[4], sx[4];
-  int mi[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    m[e] = -INFINITY;
-    mi[e] = 0x7fffffff;
+    float x[NTN];
+    float m = -INFINITY;
+    int mi = 0x7fffffff;
 #pragma unroll
     for (int tn = 0; tn < NTN; ++tn) {
       const int n = (nb * NTN + tn) * 16 + u;
-      x[e][tn] = acc[tn][e] + bn[tn];
-      if ((FULL || n < V) && x[e][tn] > m[e]) {  // columns ascend with tn: first index within the lane
-        m[e] = x[e][tn];
-        mi[e] = n;
+      x[tn] = acc[tn][e] + bn[tn];
+      if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
+        m = x[tn];
+        mi = n;
       }
     }
-  }
-  // the rows' (max, lowest column among equal maxima) over the 16 lanes of this g
-  float rm[4];
-  int ri[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) rm[e] = fmaxf(m[e], dpp_f<DPP_XOR1>(m[e]));
-#pragma unroll
-  for (int e = 0; e < 4; ++e) rm[e] = fmaxf(rm[e], dpp_f<DPP_XOR2>(rm[e]));
-#pragma unroll
-  for (int e = 0; e < 4; ++e) rm[e] = fmaxf(rm[e], dpp_f<DPP_ROR4>(rm[e]));
-#pragma unroll
-  for (int e = 0; e < 4; ++e) rm[e] = fmaxf(rm[e], dpp_f<DPP_ROR8>(rm[e]));
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    ri[e] = m[e] == rm[e] ? mi[e] : 0x7fffffff;
-    ri[e] = min(ri[e], dpp_i<DPP_XOR1>(ri[e]));
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) ri[e] = min(ri[e], dpp_i<DPP_XOR2>(ri[e]));
-#pragma unroll
-  for (int e = 0; e < 4; ++e) ri[e] = min(ri[e], dpp_i<DPP_ROR4>(ri[e]));
-#pragma unroll
-  for (int e = 0; e < 4; ++e) ri[e] = min(ri[e], dpp_i<DPP_ROR8>(ri[e]));
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    sx[e] = 0.f;
+    {  // the row's (max, lowest column among equal maxima) over the 16 lanes of this g
+      const float rm = row16_max(m);
+      mi = row16_min(m == rm ? mi : 0x7fffffff);
+      m = rm;
+    }
+    float sx = 0.f;
 #pragma unroll
     for (int tn = 0; tn < NTN; ++tn) {
       const int n = (nb * NTN + tn) * 16 + u;
-      if (FULL || n < V) sx[e] += expf(x[e][tn] - rm[e]);
+      if (n < V) sx += expf(x[tn] - m);
     }
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sx[e] += dpp_f<DPP_XOR1>(sx[e]);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sx[e] += dpp_f<DPP_XOR2>(sx[e]);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sx[e] += dpp_f<DPP_ROR4>(sx[e]);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) sx[e] += dpp_f<DPP_ROR8>(sx[e]);
-  if (u == 0) {  // lane u == 0 (the rows' first quad) writes them
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = row0 + e;
-      if (row < R) {
-        gp.mx[(size_t)row * GP_NB + nb] = rm[e];
-        gp.se[(size_t)row * GP_NB + nb] = sx[e];
-        gp.ix[(size_t)row * GP_NB + nb] = ri[e];
-      }
+    sx = row16_sum(sx);  // lane u == 0 (the row's first quad) writes it
+    const int row = row0 + e;
+    if (u == 0 && row < R) {
+      gp.mx[(size_t)row * GP_NB + nb] = m;
+      gp.se[(size_t)row * GP_NB + nb] = sx;
+      gp.ix[(size_t)row * GP_NB + nb] = mi;
     }
   }
 }
@@ -938,21 +891,11 @@ struct FoldEpi {
     // gate columns of consecutive tiles are consecutive in gates[row]; VT 16 is a multiple of 4, so
     // no segment straddles the two); the biases of the gate tiles are 0 (Pre), the stored values raw
     const bool has_gates = (nb + 1) * NTN > VT;
-    // a block of vocabulary columns only, all < V (every block but the last vocabulary one)
-    const bool full = (nb + 1) * NTN * 16 <= V && (V & 3) == 0;
-    // (CASR_DG_DIAG ablation builds only: bit 5 drops the logits stores, bit 6 the tile maxima,
-    // bit 4 the row partials)
-    float* lg = (CASR_DG_DIAG & 32) ? nullptr : logits;
-    float* tm = (CASR_DG_DIAG & 64) ? nullptr : gp.tmx;
-    if (full) {
-      if (lg || tm) proj_logits_out<NTN, true>(acc, p.bn, row0, nb, u, scr, lg, tm, R, V, VT);
-      if (gp.mx && !(CASR_DG_DIAG & 16)) proj_row_partials<NTN, true>(acc, p.bn, row0, nb, u, gp, R, V);
-      return;
-    }
-    if (lg || tm || has_gates)
-      proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, lg, tm, R, V, VT, has_gates ? gates : nullptr, 16 * VT);
+    if (logits || has_gates)
+      proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, VT, has_gates ? gates : nullptr,
+                           16 * VT);
     if (nb * NTN >= VT) return;  // no vocabulary tile in this block
-    if (gp.mx && !(CASR_DG_DIAG & 16)) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
+    if (gp.mx) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
   }
 };
 
@@ -1017,14 +960,20 @@ __global__ void fold_wq16_kernel(const float* __restrict__ w_hidden, float* __re
 }
 
 hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, float* wq16,
-                      hipStream_t s) {
+                      float* wfold32, hipStream_t s) {
   const int VT = fold_vtiles(V);
   if (VT > L.VP / 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(fold_image_kernel, dim3((VT + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w16,
-                     W + L.dec_w16, VT, wfold);
+  // the f32 and s16 fragment images share their tiling and k order (Layout), so one copy kernel
+  // assembles either fused image
+  if (wfold)
+    hipLaunchKernelGGL(fold_image_kernel, dim3((VT + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w16,
+                       W + L.dec_w16, VT, wfold);
+  if (wfold32)
+    hipLaunchKernelGGL(fold_image_kernel, dim3((VT + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w,
+                       W + L.dec_w, VT, wfold32);
   hipLaunchKernelGGL(fold_emb_gates_kernel, dim3((V + FOLD_EV - 1) / FOLD_EV, 4 * HD / 256), dim3(256), 0, s,
                      W + L.emb, W + L.dec_w, W + L.dec_b, V, emb_gates);
-  hipLaunchKernelGGL(fold_wq16_kernel, dim3((A / 16) * (HD / 64)), dim3(256), 0, s, W + L.w_hidden, wq16);
+  if (wq16) hipLaunchKernelGGL(fold_wq16_kernel, dim3((A / 16) * (HD / 64)), dim3(256), 0, s, W + L.w_hidden, wq16);
   return hipGetLastError();
 }
 
@@ -1856,11 +1805,11 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
 constexpr int FOLD_NT_BEAM = 2 * FOLD_NT;
 template <class ASrc, class Epi>
 static void launch_fold_gemm(int R, bool beam, int NB, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi,
-                             hipStream_t s) {
+                             int s16, hipStream_t s) {
   const int nkt = KPROJ / DG_BK;
-  if (!beam) {
-    if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
-    else launch_dg<4, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, 1, s);
+  if (!beam) {  // (greedy: s16x3, or the exact-f32 MFMAs on the f32 fused image)
+    if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+    else launch_dg<4, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   } else if (dec_wide(R)) {  // (128 x 224 in two rounds at R = 2048 measured 12.07 against 11.47 ms per batch)
     // A ring of three beside the W ring of two (152 KB): fused GEMM 3.96-4.02 -> 3.88-3.92 ms per beam
     // batch (interleaved A/B, two rounds; a version unrolled by 6 with static A buffers spilled 11 VGPRs)
@@ -1977,12 +1926,12 @@ static void fold_gemm_step(const DecodeArgs& a, DecodeBufs& d, int l, int total,
   const int ntiles = VT + FOLD_GT;
   const int NB = ((gates ? ntiles : VT) + NT - 1) / NT;
   ProfScope ps(a.prof, CASR_K_PROJ, s);
-  ProjA asrc{d.st[(l + 1) & 1], R, 1};
+  ProjA asrc{d.st[(l + 1) & 1], R, a.s16};
   GreedyPart gp = row_partials(a) ? d.part : GreedyPart{nullptr, nullptr, nullptr, nullptr};
   if (!beam || a.V > 16 * GP_NT) gp.tmx = nullptr;  // tile maxima: beam only
   FoldEpi epi{a.W + a.L.proj_b, d.newdone, R, a.V, VT, l, total, d.err, gp, a.fb.gates, beam ? d.logits : nullptr};
   dg_trace_step_gate(l, true, s);
-  launch_fold_gemm(R, beam, NB, ntiles, a.fb.wfold, asrc, epi, s);
+  launch_fold_gemm(R, beam, NB, ntiles, a.fb.wfold, asrc, epi, a.s16, s);
   dg_trace_step_gate(l, false, s);
 }
 

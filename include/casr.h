@@ -237,7 +237,8 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *   CASR_OPT_ATTN_DIRECT     0: attention scores in the split exponential form 1 - 2 / (1 + e^{2k}
  *                            e^{2q}) (default; one transcendental per term); 1: the
  *                            direct tanh(k + q) form the split form falls back to per block
- *   CASR_OPT_DEC_FOLD        1: greedy decode in two launches per step (s16x3; default): the
+ *   CASR_OPT_DEC_FOLD        1: greedy decode in two launches per step (default; under f32 the
+ *                            fused GEMM runs the exact-f32 MFMAs on an f32 fused image): the
  *                            projection GEMM also computes the next step's LSTM gate
  *                            pre-activations from the same [ctx | h] rows, the embedding part of
  *                            the gates is a per-token table built at bind, and the LSTM cell and

@@ -553,8 +553,8 @@ def test_decode_fold_vs_three_launches(eng, name):
     against the three-launch step (LSTMCell GEMM, attention, projection): the same arithmetic
     regrouped (decoder.py:104-114, attention.py:92, decoder.py:129-135), so identical tokens,
     lengths and finished flags, scores within 2e-3 and alignments within 1e-5; on the golden batch
-    (ragged) and at the headline size (B = 256, T = 800, all 40 steps).  Under f32 the option has no
-    effect (the fold needs the s16 images): both runs take the three-launch step."""
+    (ragged) and at the headline size (B = 256, T = 800, all 40 steps).  In both arithmetics: under
+    f32 the fused GEMM runs the exact-f32 MFMAs on the f32 fused image (round 4)."""
     def run(fold, **kw):
         eng.set_option("DEC_FOLD", fold)
         eng.profile(["dec_lstm"])
@@ -575,7 +575,7 @@ def test_decode_fold_vs_three_launches(eng, name):
         u, n_u = run(0, alignment=align)
         # the fold runs the LSTMCell GEMM at step 0 only; the three-launch step at every step
         assert n_u == CFG.max_len
-        assert n_f == (1 if eng.requested == "s16x3" else CFG.max_len)
+        assert n_f == 1
         for k in ("tokens", "out_len", "finished"):
             assert torch.equal(f[k].cpu(), u[k].cpu()), k
         np.testing.assert_allclose(f["accum"].cpu().numpy(), u["accum"].cpu().numpy(), atol=2e-3, rtol=0)

@@ -3,7 +3,10 @@
 // 4 also measured, with a templated copy of the kernel (profiles/r04/logmel/variants_r04g.txt): the
 // filter weights in registers (adopted: 7 % faster, same bits) and the stage 0 -> 1 exchange by
 // v_permlane16/32_swap (5 % faster, but hipcc then contracts the complex products differently: up to
-// 8e-3 in log-mel against the LDS form, so not adopted).  Build:
+// 8e-3 in log-mel against the LDS form, so not adopted).  With -DFE_NI and FE_SRC pointing at a copy
+// of frontend.hip whose kernel takes a second template parameter NI (frames in flight per wave,
+// interleaved through every stage) it also times NI = 2 and 4: 191 / 215 us against 181 us for
+// the default (profiles/r04/logmel/variants_ni_r04j.txt; 146 / 207 VGPRs), so not adopted.  Build:
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I chinese-asr_amd/csrc -DFE_SRC=<file> \
 //     tools/probes/logmel_variants.hip -o tools/probes/logmel_variants
 #include <hip/hip_runtime.h>
