@@ -6,7 +6,9 @@
 // 8e-3 in log-mel against the LDS form, so not adopted).  With -DFE_NI and FE_SRC pointing at a copy
 // of frontend.hip whose kernel takes a second template parameter NI (frames in flight per wave,
 // interleaved through every stage) it also times NI = 2 and 4: 191 / 215 us against 181 us for
-// the default (profiles/r04/logmel/variants_ni_r04j.txt; 146 / 207 VGPRs), so not adopted.  Build:
+// the default (profiles/r04/logmel/variants_ni_r04j.txt; 146 / 207 VGPRs), so not adopted.  With
+// -DFE_LB and a copy whose second parameter is the __launch_bounds__ minimum waves per SIMD, 5 and 6
+// waves: 253 / 412 us (36 / 51 VGPRs spilled; variants_lb_r04o.txt), not adopted.  Build:
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I chinese-asr_amd/csrc -DFE_SRC=<file> \
 //     tools/probes/logmel_variants.hip -o tools/probes/logmel_variants
 #include <hip/hip_runtime.h>
@@ -32,7 +34,8 @@ using namespace casr;
     }                                                                              \
   } while (0)
 
-#ifdef FE_NI  // a kernel source with the frames-in-flight parameter (log_mel_kernel<FPW, NI>)
+#if defined(FE_NI) || defined(FE_LB)  // a kernel source with a second template parameter
+                                     // (frames in flight, or the minimum waves per SIMD)
 #define FE_KERNEL(FPW, NI) log_mel_kernel<FPW, NI>
 #else
 #define FE_KERNEL(FPW, NI) log_mel_kernel<FPW>
@@ -103,6 +106,12 @@ int main() {
   run<8>("v0 FPW 8 (default)", wav, nsd, B, N, T, k, out, fr, err, nullptr, &ref);
   run<4>("v1 FPW 4", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
   run<16>("v2 FPW 16", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+#ifdef FE_LB  // log_mel_kernel<FPW, MINW>: __launch_bounds__(256, MINW)
+  run<8, 5>("v3 FPW 8, 5 waves per SIMD", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+  run<8, 6>("v4 FPW 8, 6 waves per SIMD", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+  run<16, 5>("v5 FPW 16, 5 waves per SIMD", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+  run<16, 6>("v6 FPW 16, 6 waves per SIMD", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
+#endif
 #ifdef FE_NI
   run<8, 2>("v3 FPW 8, 2 frames in flight", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
   run<16, 2>("v4 FPW 16, 2 frames in flight", wav, nsd, B, N, T, k, out, fr, err, &ref, nullptr);
