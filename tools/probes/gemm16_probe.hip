@@ -67,7 +67,7 @@ int main() {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char* names[6] = {"bias_kernel<4>", "persist", "p:no-dma", "p:iglp1", "p:prio", "p:iglp1+prio"};
+    const char* names[6] = {"bias_kernel<4>", "persist", "p:no-dma", "p:no-mfma", "p:no-stores", "p:dma-only"};
     float* outs[6] = {dC0, dC1, dC1, dC1, dC1, dC1};
     for (int rep = 0; rep < 3; ++rep)
       for (int v = 0; v < 6; ++v) {
@@ -88,13 +88,13 @@ int main() {
             hipLaunchKernelGGL(gemm16_persist_kernel<1>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
                                order, order.blocks(), Kp / G16_K);
           else if (v == 3)
-            hipLaunchKernelGGL(gemm16_persist_kernel<8>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
+            hipLaunchKernelGGL(gemm16_persist_kernel<2>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
                                order, order.blocks(), Kp / G16_K);
           else if (v == 4)
-            hipLaunchKernelGGL(gemm16_persist_kernel<16>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
+            hipLaunchKernelGGL(gemm16_persist_kernel<4>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
                                order, order.blocks(), Kp / G16_K);
           else
-            hipLaunchKernelGGL(gemm16_persist_kernel<24>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
+            hipLaunchKernelGGL(gemm16_persist_kernel<6>, dim3(256), dim3(512), 0, 0, dA, dW, dB, outs[v], M, N, Kp,
                                order, order.blocks(), Kp / G16_K);
         }
         CK(hipEventRecord(e1));
