@@ -460,8 +460,9 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
   h->dec_small = info[5] == 1.f;
   h->W = packed_device;
   h->graphs.clear();  // captured graphs bake in the precision and weight pointers
-  // the folded greedy step's tables (decoder.hip build_fold): derived from this blob, so rebuilt
-  // at every bind; a blob without valid s16 images keeps the three-launch step
+  // the folded step's tables (decoder.hip build_fold): derived from this blob, so rebuilt at every
+  // bind; the f32 fused image and the gate table always (the greedy fold under f32), the s16 fused
+  // image and the s16 query image only from a blob with valid s16 images
   h->fold_ready = h->fold32_ready = false;
   {
     const int V = h->cfg.vocab;
