@@ -466,7 +466,7 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
   h->fold_ready = h->fold32_ready = false;
   {
     const int V = h->cfg.vocab;
-    const size_t img = (size_t)(fold_vtiles(V) + FOLD_GT) * (KPROJ / 64) * FRAG * sizeof(float);
+    const size_t img = (size_t)(fold_gtile0(V) + FOLD_GT) * (KPROJ / 64) * FRAG * sizeof(float);
     HIP_OK(h, h->wfold32.ensure(img));
     HIP_OK(h, h->egates.ensure((size_t)V * 4 * HD * sizeof(float)));
     if (h->s16_valid) {

@@ -311,10 +311,14 @@ __device__ __forceinline__ void greedy_book(const GreedySel& gs, int r, int t, f
 constexpr int FOLD_GT = 4 * HD / 16;  // LSTM gate tiles (16 gate rows each) in the fused image
 constexpr int FOLD_NT = 7;            // 16-column tiles per fused GEMM block (112 columns)
 inline int fold_vtiles(int V) { return (V + 15) / 16; }
+// (round 4) the gate tiles of the fused image start at the vocabulary tiles rounded up to a whole
+// 7-tile wave column (zero tiles between): no wave column holds both vocabulary and gate tiles, so
+// the fused GEMM's epilogue has no mixed column, the one that ended last
+inline int fold_gtile0(int V) { return (fold_vtiles(V) + FOLD_NT - 1) / FOLD_NT * FOLD_NT; }
 constexpr size_t FOLD_WQ16_FLOATS = (size_t)A * HD;  // the W_hidden fragment image (beam query)
 struct FoldBufs {
   const float* wfold;      // fragment image (s16, or f32 under the exact-f32 arithmetic):
-                           // [fold_vtiles(V) + FOLD_GT tiles][KPROJ / 64] FRAG blocks
+                           // [fold_gtile0(V) + FOLD_GT tiles][KPROJ / 64] FRAG blocks
   const float* emb_gates;  // [V][4 HD] packed gate-row order (packed_gate_row), biases included
   const float* wq16;       // s16 fragment image of W_hidden^T: [A / 16 tiles][HD / 64] FRAG blocks
   float* gates;            // [R][4 HD] the next step's [ctx | h] . W_ch^T, packed gate-row order

@@ -868,6 +868,7 @@ struct FoldEpi {
   GreedyPart gp;   // row partials (greedy; beam at temperature 1) or gp.mx == nullptr
   float* gates;    // [R][4 HD]
   float* logits;   // [R][V] (beam), or nullptr
+  int VG;          // first gate tile (fold_gtile0: VT rounded up to a whole wave column)
   struct Pre {
     float bn[16];
   };
@@ -890,26 +891,28 @@ struct FoldEpi {
     // logits (beam) and the gate columns through the wave's LDS slab as float4 row segments (the
     // gate columns of consecutive tiles are consecutive in gates[row]; VT 16 is a multiple of 4, so
     // no segment straddles the two); the biases of the gate tiles are 0 (Pre), the stored values raw
-    const bool has_gates = (nb + 1) * NTN > VT;
+    const bool has_gates = (nb + 1) * NTN > VG;
     if (logits || has_gates)
       proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, VT, has_gates ? gates : nullptr,
-                           16 * VT);
+                           16 * VG);
     if (nb * NTN >= VT) return;  // no vocabulary tile in this block
     if (gp.mx) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
   }
 };
 
 // ------------------------------------------------------------------ fold tables (bind time)
-// the fused fragment image: vocabulary tiles 0..VT-1 of proj_w16, then the 128 LSTM gate tiles of
-// dec_w16 restricted to its k blocks 4..19 (the [ctx | h] part of [emb | ctx | h]: E = 256 = 4 x 64)
-__global__ void fold_image_kernel(const float* __restrict__ proj16, const float* __restrict__ dec16, int VT,
+// the fused fragment image: vocabulary tiles 0..VT-1 of proj_w16, zero tiles up to VG (a whole wave
+// column), then the 128 LSTM gate tiles of dec_w16 restricted to its k blocks 4..19 (the [ctx | h]
+// part of [emb | ctx | h]: E = 256 = 4 x 64)
+__global__ void fold_image_kernel(const float* __restrict__ proj16, const float* __restrict__ dec16, int VT, int VG,
                                   float* __restrict__ out) {
   const int T = blockIdx.x / (KPROJ / 64), kc = blockIdx.x % (KPROJ / 64);
-  const float* src = T < VT ? proj16 + ((size_t)T * (KPROJ / 64) + kc) * FRAG
-                            : dec16 + ((size_t)(T - VT) * (KDEC / 64) + E / 64 + kc) * FRAG;
+  const float* src = T < VT   ? proj16 + ((size_t)T * (KPROJ / 64) + kc) * FRAG
+                     : T < VG ? nullptr
+                              : dec16 + ((size_t)(T - VG) * (KDEC / 64) + E / 64 + kc) * FRAG;
   float* dst = out + (size_t)blockIdx.x * FRAG;
   for (int i = threadIdx.x; i < FRAG / 4; i += blockDim.x)
-    reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+    reinterpret_cast<float4*>(dst)[i] = src ? reinterpret_cast<const float4*>(src)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // the per-token gate table: emb_gates[v][n] = sum_k emb[v][k] W_dec[n][k] (k < E, f32 fma chain
@@ -961,16 +964,16 @@ __global__ void fold_wq16_kernel(const float* __restrict__ w_hidden, float* __re
 
 hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, float* wq16,
                       float* wfold32, hipStream_t s) {
-  const int VT = fold_vtiles(V);
+  const int VT = fold_vtiles(V), VG = fold_gtile0(V);
   if (VT > L.VP / 16) return hipErrorInvalidValue;
   // the f32 and s16 fragment images share their tiling and k order (Layout), so one copy kernel
   // assembles either fused image
   if (wfold)
-    hipLaunchKernelGGL(fold_image_kernel, dim3((VT + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w16,
-                       W + L.dec_w16, VT, wfold);
+    hipLaunchKernelGGL(fold_image_kernel, dim3((VG + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w16,
+                       W + L.dec_w16, VT, VG, wfold);
   if (wfold32)
-    hipLaunchKernelGGL(fold_image_kernel, dim3((VT + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w,
-                       W + L.dec_w, VT, wfold32);
+    hipLaunchKernelGGL(fold_image_kernel, dim3((VG + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w,
+                       W + L.dec_w, VT, VG, wfold32);
   hipLaunchKernelGGL(fold_emb_gates_kernel, dim3((V + FOLD_EV - 1) / FOLD_EV, 4 * HD / 256), dim3(256), 0, s,
                      W + L.emb, W + L.dec_w, W + L.dec_b, V, emb_gates);
   if (wq16) hipLaunchKernelGGL(fold_wq16_kernel, dim3((A / 16) * (HD / 64)), dim3(256), 0, s, W + L.w_hidden, wq16);
@@ -1921,15 +1924,15 @@ void dg_trace_dump() {
 static void fold_gemm_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, hipStream_t s) {
   const int R = a.B * a.k;
   const bool beam = !a.greedy_run;
-  const int VT = fold_vtiles(a.V), NT = beam ? FOLD_NT_BEAM : FOLD_NT;
+  const int VT = fold_vtiles(a.V), VG = fold_gtile0(a.V), NT = beam ? FOLD_NT_BEAM : FOLD_NT;
   const bool gates = l + 1 < a.max_len;
-  const int ntiles = VT + FOLD_GT;
+  const int ntiles = VG + FOLD_GT;
   const int NB = ((gates ? ntiles : VT) + NT - 1) / NT;
   ProfScope ps(a.prof, CASR_K_PROJ, s);
   ProjA asrc{d.st[(l + 1) & 1], R, a.s16};
   GreedyPart gp = row_partials(a) ? d.part : GreedyPart{nullptr, nullptr, nullptr, nullptr};
   if (!beam || a.V > 16 * GP_NT) gp.tmx = nullptr;  // tile maxima: beam only
-  FoldEpi epi{a.W + a.L.proj_b, d.newdone, R, a.V, VT, l, total, d.err, gp, a.fb.gates, beam ? d.logits : nullptr};
+  FoldEpi epi{a.W + a.L.proj_b, d.newdone, R, a.V, VT, l, total, d.err, gp, a.fb.gates, beam ? d.logits : nullptr, VG};
   dg_trace_step_gate(l, true, s);
   launch_fold_gemm(R, beam, NB, ntiles, a.fb.wfold, asrc, epi, a.s16, s);
   dg_trace_step_gate(l, false, s);
