@@ -225,18 +225,18 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       const int cnt = newdone[min(ln, lm - 1)];
       const int pi = r * GP_NB + min(ln, max(gs.nbp - 1, 0));
       float m = 0.f, se = 0.f;
-      int mi = 0, tq = 0, bkv = 0;
+      int mi = 0, tq = 0, bkv = 0, finv = 0;
       if (cell.sel) {
         m = gs.gp.mx[pi];
         se = gs.gp.se[pi];
         mi = gs.gp.ix[pi];
-        // the row's bookkeeping words in lanes 0..2 of one load: the dword holding fin[r], accum[r],
-        // out_len[r] (a per-lane address, so hipcc makes no early scalar copy of them, whose wait
-        // would sit in front of the W_hidden loads)
-        const int32_t* bk = ln == 1   ? reinterpret_cast<const int32_t*>(gs.accum + r)
-                            : ln == 2 ? gs.out_len + r
-                                      : reinterpret_cast<const int32_t*>(gs.fin + (r & ~3));
+        // the row's bookkeeping words: accum[r] in lane 1, out_len[r] in the others, from one load
+        // (a per-lane address, so hipcc makes no early scalar copy of them, whose wait would sit in
+        // front of the W_hidden loads), and fin[r] by a byte load beside it (the caller's B-byte
+        // finished buffer: no alignment or padding is assumed)
+        const int32_t* bk = ln == 1 ? reinterpret_cast<const int32_t*>(gs.accum + r) : gs.out_len + r;
         bkv = *bk;
+        finv = gs.fin[r];
       } else {
         tq = cell.tok[r];
       }
@@ -256,9 +256,9 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
           const bool bad_t = (unsigned)t >= (unsigned)V;  // no finite maximum (NaN row)
           if (bad_t) t = 0;
           const float sx = wave_sum((se > 0.f) ? se * expf(m - gm) : 0.f);
-          const uint8_t fin0 = (uint8_t)((uint32_t)__builtin_amdgcn_readlane(bkv, 0) >> (8 * (r & 3)));
+          const uint8_t fin0 = (uint8_t)__builtin_amdgcn_readfirstlane(finv);
           const float acc0 = __int_as_float(__builtin_amdgcn_readlane(bkv, 1));
-          const int len0 = __builtin_amdgcn_readlane(bkv, 2);
+          const int len0 = __builtin_amdgcn_readlane(bkv, 0);
           if (ln == 0) {
             if (bad_t) atomicOr(cell.err, CASR_DEV_NAN_LOGITS);
             greedy_book(gs, r, t, gm - (logf(sx) + gm), fin0, acc0, len0);

@@ -461,24 +461,35 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
   h->W = packed_device;
   h->graphs.clear();  // captured graphs bake in the precision and weight pointers
   // the folded step's tables (decoder.hip build_fold): derived from this blob, so rebuilt at every
-  // bind; the f32 fused image and the gate table always (the greedy fold under f32), the s16 fused
-  // image and the s16 query image only from a blob with valid s16 images
+  // bind; the gate table always, the s16 fused image and the s16 query image only from a blob with
+  // valid s16 images.  The f32 fused image (29 MB, read only by the greedy fold under the exact-f32
+  // arithmetic) is built by the first such decode (ensure_fold32)
   h->fold_ready = h->fold32_ready = false;
   {
     const int V = h->cfg.vocab;
-    const size_t img = (size_t)(fold_gtile0(V) + FOLD_GT) * (KPROJ / 64) * FRAG * sizeof(float);
-    HIP_OK(h, h->wfold32.ensure(img));
     HIP_OK(h, h->egates.ensure((size_t)V * 4 * HD * sizeof(float)));
     if (h->s16_valid) {
-      HIP_OK(h, h->wfold.ensure(img));
+      HIP_OK(h, h->wfold.ensure(fold_image_bytes(V)));
       HIP_OK(h, h->wq16.ensure(FOLD_WQ16_FLOATS * sizeof(float)));
     }
     HIP_OK(h, build_fold(h->W, h->L, V, h->s16_valid ? h->wfold.as<float>() : nullptr, h->egates.as<float>(),
-                         h->s16_valid ? h->wq16.as<float>() : nullptr, h->wfold32.as<float>(), nullptr));
+                         h->s16_valid ? h->wq16.as<float>() : nullptr, nullptr, nullptr));
     HIP_OK(h, hipStreamSynchronize(nullptr));
     h->fold_ready = h->s16_valid;
-    h->fold32_ready = true;
   }
+  return CASR_OK;
+}
+
+// the f32 fused image of the folded greedy step under the exact-f32 arithmetic, built once per bind
+// by the first decode that needs it (on the null stream, synchronised: a decode's captured graph
+// never contains the build)
+static int ensure_fold32(casr_handle* h) {
+  if (h->fold32_ready) return CASR_OK;
+  const int V = h->cfg.vocab;
+  HIP_OK(h, h->wfold32.ensure(fold_image_bytes(V)));
+  HIP_OK(h, build_fold(h->W, h->L, V, nullptr, nullptr, nullptr, h->wfold32.as<float>(), nullptr));
+  HIP_OK(h, hipStreamSynchronize(nullptr));
+  h->fold32_ready = true;
   return CASR_OK;
 }
 
@@ -934,6 +945,10 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a, bool greedy) {
   const bool fold_len = !greedy || L <= 64;
   // greedy folds in either arithmetic (round 4: the exact-f32 MFMAs on the f32 fused image); the
   // beam fold's one-accumulator shapes and its s16 query need the s16 images
+  if (!a.s16 && greedy && h->W && h->tune[CASR_OPT_DEC_FOLD] && fold_vocab && fold_lds && fold_len) {
+    const int rc = ensure_fold32(h);
+    if (rc) return rc;
+  }
   const bool fold_arith = a.s16 ? h->fold_ready : (greedy && h->fold32_ready);
   a.fold = (greedy || fold_beam) && fold_vocab && fold_lds && fold_len && fold_arith && h->tune[CASR_OPT_DEC_FOLD] ? 1 : 0;
   if (a.fold) {

@@ -315,6 +315,8 @@ inline int fold_vtiles(int V) { return (V + 15) / 16; }
 // 7-tile wave column (zero tiles between): no wave column holds both vocabulary and gate tiles, so
 // the fused GEMM's epilogue has no mixed column, the one that ended last
 inline int fold_gtile0(int V) { return (fold_vtiles(V) + FOLD_NT - 1) / FOLD_NT * FOLD_NT; }
+// bytes of one fused image (s16 or f32: the same tiling)
+inline size_t fold_image_bytes(int V) { return (size_t)(fold_gtile0(V) + FOLD_GT) * (KPROJ / 64) * FRAG * sizeof(float); }
 constexpr size_t FOLD_WQ16_FLOATS = (size_t)A * HD;  // the W_hidden fragment image (beam query)
 struct FoldBufs {
   const float* wfold;      // fragment image (s16, or f32 under the exact-f32 arithmetic):
@@ -323,9 +325,9 @@ struct FoldBufs {
   const float* wq16;       // s16 fragment image of W_hidden^T: [A / 16 tiles][HD / 64] FRAG blocks
   float* gates;            // [R][4 HD] the next step's [ctx | h] . W_ch^T, packed gate-row order
 };
-// build the fused images and the per-token gate table from a bound blob (bind time): wfold and
-// wq16 from the s16 images (nullptr: skipped, a blob without valid s16 images), wfold32 from the f32
-// fragment images (the folded greedy step under the exact-f32 arithmetic), emb_gates always
+// build the fused images and the per-token gate table from a bound blob: wfold and wq16 from the s16
+// images, wfold32 from the f32 fragment images (the folded greedy step under the exact-f32
+// arithmetic), emb_gates from the embedding and the decoder LSTM weights; each nullptr is skipped
 hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, float* wq16,
                       float* wfold32, hipStream_t s);
 

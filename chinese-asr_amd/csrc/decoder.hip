@@ -974,8 +974,9 @@ hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, floa
   if (wfold32)
     hipLaunchKernelGGL(fold_image_kernel, dim3((VG + FOLD_GT) * (KPROJ / 64)), dim3(256), 0, s, W + L.proj_w,
                        W + L.dec_w, VT, VG, wfold32);
-  hipLaunchKernelGGL(fold_emb_gates_kernel, dim3((V + FOLD_EV - 1) / FOLD_EV, 4 * HD / 256), dim3(256), 0, s,
-                     W + L.emb, W + L.dec_w, W + L.dec_b, V, emb_gates);
+  if (emb_gates)
+    hipLaunchKernelGGL(fold_emb_gates_kernel, dim3((V + FOLD_EV - 1) / FOLD_EV, 4 * HD / 256), dim3(256), 0, s,
+                       W + L.emb, W + L.dec_w, W + L.dec_b, V, emb_gates);
   if (wq16) hipLaunchKernelGGL(fold_wq16_kernel, dim3((A / 16) * (HD / 64)), dim3(256), 0, s, W + L.w_hidden, wq16);
   return hipGetLastError();
 }
@@ -1898,6 +1899,10 @@ static void dg_trace_step_gate(int l, bool before, hipStream_t s) {
   static const int step = std::getenv("CASR_DG_TRACE_STEP") ? std::atoi(std::getenv("CASR_DG_TRACE_STEP")) : -1;
   uint32_t* buf = dg_trace_buffer();
   if (!buf || step < 0) return;
+  // a pageable host-to-device copy inside a stream capture could be refused or invalidate the
+  // graph: the step gate applies to eager decodes only (diagnostics)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return;
   static uint32_t* on = nullptr;
   static uint32_t* const off = nullptr;
   on = buf;

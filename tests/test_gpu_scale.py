@@ -255,6 +255,67 @@ def test_config5_beam16_lm_b1024_sharded_matches_oracle(prec):
     assert len(flips) <= (1 if prec == "f32" else 0), flips
 
 
+@pytest.mark.parametrize("prec", ["s16x3", "f32"])
+def test_config5_beam16_lm_whole_shard_final_output_matches_oracle(prec):
+    """BASELINE config 5's final answers, end to end, on one whole shard: beam 16 + second pass
+    (StubLM, lm_weight = length_weight = 1.5, main.py:45-51), EOS-bias weights, T = 800, B = 64
+    (R = 1024 decode rows: the folded beam step under s16x3, 4 of an utterance's 16 rows per
+    attention block), against O.beam_decode(..., 16, second_pass=True) on the SAME 64 utterances.
+    The reference's beam stops only when every utterance of its batch has had an EOS top candidate
+    (model.py:897-901), and the second pass chooses among the records of every step the batch ran
+    (model.py:749-763; the unfinished fallback adds length_weight * (l + 1), :961-972), so only the
+    same batch on both sides pins the answer the product returns.  Checked for all 64 utterances:
+      * the loop's step count equals the oracle's;
+      * every finished-hypothesis record (step, rank order) equals the oracle's: tokens identical,
+        scores 2e-3;
+      * the final answer (Engine.beam's unfinished fallback, replaced by second_pass_select over the
+        device records wherever an utterance has records, as Model.eval_one_batch_with_beam does):
+        tokens identical, score 2e-3.
+    Near ties: in the exact-f32 arithmetic one utterance may split at a near-tied pruning step
+    (near_tie_records_check: the records before the split identical, both diverging hypotheses
+    rescored by the oracle to their own scores); that utterance's answer is then not compared.
+    The s16x3 arithmetic (the default) must match every utterance."""
+    from casr.engine import Engine
+    from casr.results import records_by_utterance, second_pass_select
+    from golden_util import near_tie_records_check, teacher_forced_score
+    from stub_lm import StubLM, pua_int2word
+    B, k = 64, 16
+    lm, i2w = StubLM(), pua_int2word(CFG.vocab)
+    e = Engine(CFG, *eos_weights())
+    e.set_precision(prec)
+    try:
+        e.encode_fbank(torch.from_numpy(_fbank(B)).to(e.device),
+                       torch.full((B,), T_BENCH, dtype=torch.int32, device=e.device))
+        e.profile(["dec_lstm"])
+        r = e.beam(k, 1.5, 1.5)
+        n_lstm = e.profile_read()["dec_lstm"][0]
+        e.profile([])
+        bt, bl, bs, st = (t.cpu().numpy() for t in (r["tokens"], r["length"], r["score"], r["steps"]))
+        recs = records_by_utterance(*(x.cpu().numpy() for x in e.beam_records()))
+        assert e.device_flags() == 0
+    finally:
+        e.close()
+    assert n_lstm == (1 if prec == "s16x3" else CFG.max_len)  # which decode step ran
+    best = {b: (bt[b, :bl[b]].tolist(), float(bs[b])) for b in range(B)}
+    best.update(second_pass_select(recs, i2w, lm, 1.5, 1.5))
+    ref = oracle_beam_lm(tuple(range(B)), k)
+    assert int(st[0]) == ref["steps"]
+    flips, n_rec = [], 0
+    for b in range(B):
+        mine, gold = recs.get(b, []), ref["records"][b]
+        n_rec += len(gold)
+        feat = O.features_from_fbank(fbank_for(b, T_BENCH))
+        rescore = lambda t, feat=feat: teacher_forced_score(feat, t + [CFG.eos], *eos_weights())
+        if not near_tie_records_check(mine, gold, 2e-3, rescore):
+            flips.append(b)
+            continue
+        assert best[b][0] == ref["tokens"][b], b
+        assert abs(best[b][1] - ref["score"][b]) <= 2e-3, (b, best[b][1], ref["score"][b])
+    assert n_rec > 1000  # the shard exercises the second pass (> 1 record) and the fallback (none)
+    assert any(len(v) > 1 for v in ref["records"].values()) and any(not v for v in ref["records"].values())
+    assert len(flips) <= (1 if prec == "f32" else 0), flips
+
+
 @pytest.mark.parametrize("name", ["plain", "peaked"])
 @pytest.mark.parametrize("k", [4, 8])
 def test_beam_temperature_matches_reference(name, k):

@@ -1,45 +1,92 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel stats.
-# Each GPU step has its own time limit; a fault / abort / timeout stops the session.
+# One GPU-box session, parameterised (replaces the per-round tools/gpu_r0*.sh scripts).
+#
+#   OUT=gpurun_out/<tag> STAGES="smoke tests suite bench" bash tools/gpu_session.sh
+#
+# Stages, run in the order given; each GPU step has its own time limit, and a fault, abort,
+# segfault or time-out stops the session (no further GPU step after it):
+#   smoke            __graft_entry__.smoke()
+#   tests            pytest -m gpu on TESTS (files / node ids, default: the whole tests/ tree),
+#                    filtered by TESTS_K (pytest -k) when set
+#   suite            the whole -m gpu suite (as the driver runs it, -x)
+#   bench            python bench.py $BENCH_ARGS > $OUT/bench.json
+#   ab               interleaved A/B: for each of AB_ROUNDS rounds, bench.py $AB_ARGS once per
+#                    CASR_OPTS value in AB_OPTS (';'-separated; "-" = defaults) -> $OUT/ab_<i>_<r>.json
+#   counters         rocprofv3 -L (the counters this box can collect) -> $OUT/counters.txt
+#   pmc              PMC passes of tools/probes/one_step.py (PMC_MODES: greedy and/or beam) with the
+#                    counter sets in PMC_SETS (';'-separated passes); ordinary recurrence launch
+#                    (REC_COOP=0, DESIGN 3.2: a cooperative launch ends in SIGSEGV under rocprofv3)
+#   trace            tools/rec_trace.py
+#   prof             rocprofv3 kernel trace + stats of bench.py (greedy only) on the shipped
+#                    cooperative launch; its exit status is recorded (must be the LAST stage)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out
-mkdir -p $OUT
-STAGES="${STAGES:-pytest smoke bench prof}"
+OUT=${OUT:-gpurun_out/session}
+mkdir -p "$OUT"
+STAGES="${STAGES:-smoke suite bench}"
 FAULT_RE='illegal memory access|HSA_STATUS_ERROR|Memory access fault|hipErrorIllegalAddress|core dumped|Aborted'
-stop_on_fault() {  # $1 = rc, $2 = stage, $3 = log
+stop_on() {  # $1 = rc, $2 = stage, $3 = log
   if [ -n "$3" ] && grep -Eq "$FAULT_RE" "$3"; then
     echo "[$2] GPU fault in $3: stopping the session"; exit 99
   fi
-  case "$1" in
-    0) return 0 ;;
-    1) [ "$2" = pytest ] && { echo "[$2] test failures (rc=1), continuing"; return 0; } ;;
-  esac
-  echo "[$2] rc=$1: stopping the session"; exit "$1"
+  [ "$1" = 0 ] && return 0
+  echo "[$2] rc=$1: stopping the session"; tail -30 "$3"; exit "$1"
 }
+PYTEST="python -u -m pytest -x -v --timeout ${TEST_TIMEOUT:-300} --timeout-method thread -p no:cacheprovider"
 for s in $STAGES; do
   case $s in
-    pytest)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
-      rc=$?; tail -5 $OUT/pytest_gpu.log; stop_on_fault $rc pytest $OUT/pytest_gpu.log ;;
-    pytestall)
-      timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
-      rc=$?; tail -15 $OUT/pytest_gpu.log; stop_on_fault $rc pytest $OUT/pytest_gpu.log ;;
     smoke)
-      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
-      rc=$?; tail -3 $OUT/smoke.log; stop_on_fault $rc smoke $OUT/smoke.log ;;
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
+      rc=$?; tail -1 $OUT/smoke.log; stop_on $rc smoke $OUT/smoke.log ;;
+    tests)
+      timeout -k 10 ${TESTS_LIMIT:-900} $PYTEST -m gpu ${TESTS:-tests} ${TESTS_K:+-k "$TESTS_K"} > $OUT/tests.log 2>&1
+      rc=$?; grep -E "PASSED|FAILED|ERROR|SKIPPED" $OUT/tests.log | sed 's/^tests\///' | tail -60; tail -1 $OUT/tests.log
+      stop_on $rc tests $OUT/tests.log ;;
+    suite)
+      timeout -k 10 1000 $PYTEST -m gpu tests > $OUT/pytest_gpu.log 2>&1
+      rc=$?; tail -1 $OUT/pytest_gpu.log; stop_on $rc suite $OUT/pytest_gpu.log ;;
     bench)
       timeout -k 10 600 python bench.py ${BENCH_ARGS} > $OUT/bench.json 2> $OUT/bench.err
-      rc=$?; cat $OUT/bench.json; tail -3 $OUT/bench.err; stop_on_fault $rc bench $OUT/bench.err ;;
-    prof)
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-        python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-configs ${PROF_ARGS} > $OUT/prof_bench.json 2> $OUT/prof.err
-      rc=$?; tail -3 $OUT/prof.err; stop_on_fault $rc prof $OUT/prof.err
-      python tools/prof_by_grid.py $OUT/prof/run_kernel_trace.csv 30 > $OUT/prof_by_grid.txt 2>&1
-      head -12 $OUT/prof_by_grid.txt ;;
+      rc=$?; stop_on $rc bench $OUT/bench.err
+      python tools/bench_line.py $OUT/bench.json ;;
+    ab)
+      IFS=';' read -r -a opts <<< "${AB_OPTS:--}"
+      for r in $(seq 1 ${AB_ROUNDS:-2}); do
+        for i in "${!opts[@]}"; do
+          o="${opts[$i]}"; [ "$o" = "-" ] && o=""
+          CASR_OPTS="$o" timeout -k 10 300 python bench.py --steps ${AB_STEPS:-20} --warmup 3 --no-configs \
+            --no-cpu-baseline --no-f32-compare ${AB_ARGS} > $OUT/ab_${i}_$r.json 2> $OUT/ab.err
+          rc=$?; stop_on $rc ab $OUT/ab.err
+          echo -n "[$r] opts='$o' "; python tools/bench_line.py $OUT/ab_${i}_$r.json
+        done
+      done ;;
+    counters)
+      timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1
+      rc=$?; grep -ciE "counter|name" $OUT/counters.txt; stop_on $rc counters $OUT/counters.txt ;;
+    pmc)
+      IFS=';' read -r -a sets <<< "${PMC_SETS:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE;FETCH_SIZE;WRITE_SIZE}"
+      for mode in ${PMC_MODES:-greedy beam}; do
+        P=$OUT/pmc_$mode
+        mkdir -p $P
+        if [ $mode = beam ]; then export BEAM=8 B=256; else unset BEAM; export B=256; fi
+        for i in "${!sets[@]}"; do
+          CASR_OPTS=REC_COOP=0 timeout -s KILL 120 rocprofv3 --pmc ${sets[$i]} --output-format csv -d $P/p$i -o p$i -- \
+            python3 tools/probes/one_step.py > $P/p$i.log 2>&1
+          rc=$?; stop_on $rc "pmc $mode ${sets[$i]}" $P/p$i.log
+        done
+      done
+      unset BEAM B ;;
     trace)
       timeout -k 10 300 python tools/rec_trace.py > $OUT/rec_trace.txt 2>&1
-      rc=$?; cat $OUT/rec_trace.txt; stop_on_fault $rc trace $OUT/rec_trace.txt ;;
+      rc=$?; tail -20 $OUT/rec_trace.txt; stop_on $rc trace $OUT/rec_trace.txt ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+        python3 bench.py --steps 20 --warmup 2 --no-beam --no-configs --no-f32-compare --no-cpu-baseline \
+        > $OUT/prof_bench.json 2> $OUT/prof.err
+      echo "rocprofv3 kernel trace of the default (cooperative) launch: exit status $?" | tee $OUT/prof_rc.txt
+      python tools/prof_by_grid.py $OUT/prof/run_kernel_trace.csv 30 > $OUT/prof_by_grid.txt 2>&1
+      head -14 $OUT/prof_by_grid.txt
+      break ;;
   esac
 done
 echo "session done"
