@@ -833,15 +833,28 @@ hipError_t launch_attention_step(const DecodeArgs& a, float* st, const float* qp
   }
 }
 
+// the kernel's static LDS (its __shared__ words: 256-336 B), read once from the code object
+template <int KPB, int CELL = 0>
+static size_t attn_static_bytes() {
+  static const size_t v = [] {
+    hipFuncAttributes fa{};
+    const hipError_t e = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(attention_kernel<KPB, CELL>));
+    return e == hipSuccess ? (size_t)fa.sharedSizeBytes : (size_t)1024;
+  }();
+  return v;
+}
+
+// LDS of one attention block without the value prefetch (which takes what is left): the dynamic
+// area plus the kernel's static words, against the 160 KiB a workgroup may hold
 size_t attention_smem_bytes(int B, int k, int Tp, int opt, int cell) {
-  size_t f;
   switch (attention_kpb(B, k, opt)) {
-    case 1: f = cell == 1 ? attn_smem_floats<1, 1>(Tp) : attn_smem_floats<1>(Tp); break;
-    case 2: f = attn_smem_floats<2>(Tp); break;
-    case 8: f = attn_smem_floats<8>(Tp); break;
-    default: f = attn_smem_floats<4>(Tp); break;
+    case 1:
+      return cell == 1 ? attn_smem_floats<1, 1>(Tp) * sizeof(float) + attn_static_bytes<1, 1>()
+                       : attn_smem_floats<1>(Tp) * sizeof(float) + attn_static_bytes<1>();
+    case 2: return attn_smem_floats<2>(Tp) * sizeof(float) + attn_static_bytes<2>();
+    case 8: return attn_smem_floats<8>(Tp) * sizeof(float) + attn_static_bytes<8>();
+    default: return attn_smem_floats<4>(Tp) * sizeof(float) + attn_static_bytes<4>();
   }
-  return f * sizeof(float);
 }
 
 void attn_trace_bind(uint32_t* buf) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_at_trace), &buf, sizeof(buf)); }

@@ -86,8 +86,10 @@ def test_greedy_max_len_64_still_folds(prec):
 
 # The folded greedy attention (attention_kernel<1, 1>) holds its cell area (AT_CELL_FLOATS = 2560
 # floats) on top of the three-launch attention's LDS, 560 + 9 Tq floats at KPB = 1 (attention.hip
-# attn_smem_floats): the folded form fits 160 KiB up to Tq = 4204, the three-launch form up to 4488.
-# T = 12900 frames (Tp = 4300, 129 s of audio) lies between the two.
+# attn_smem_floats), plus 320-336 B of static __shared__ words: the folded form fits 160 KiB up to
+# Tq = 4195, the three-launch form up to 4488.  T = 12900 frames (Tp = 4300, 129 s of audio) lies
+# between the two.  (Round 5: the guard first counted the dynamic area only, so Tp = 4200 passed it
+# and the launch was refused with 164,016 B; attention_smem_bytes now adds the static words.)
 @pytest.mark.parametrize("prec", PRECS)
 def test_greedy_long_utterance_past_fold_lds_takes_three_launch_step(prec):
     """An utterance of Tp = 4300 encoder frames: the folded attention's LDS would exceed 160 KiB,
@@ -99,8 +101,17 @@ def test_greedy_long_utterance_past_fold_lds_takes_three_launch_step(prec):
 
 @pytest.mark.parametrize("prec", PRECS)
 def test_greedy_long_utterance_below_fold_lds_still_folds(prec):
-    """Tp = 4200 (T = 12600): the folded attention still fits, one LSTMCell launch; oracle tokens."""
-    _greedy_vs_oracle(CasrConfig(), [12600, 11000], prec, want_lstm=1)
+    """Tp = 4180 (T = 12540): the folded attention still fits (163,296 B), one LSTMCell launch;
+    oracle tokens."""
+    _greedy_vs_oracle(CasrConfig(), [12540, 11000], prec, want_lstm=1)
+
+
+@pytest.mark.parametrize("prec", PRECS)
+def test_greedy_long_utterance_at_fold_lds_edge_takes_three_launch_step(prec):
+    """Tp = 4200 (T = 12600): 163,680 B of dynamic LDS fit 160 KiB, but not with the kernel's 336 B
+    of static LDS; the guard counts both and keeps the three-launch step (the launch itself would
+    be refused)."""
+    _greedy_vs_oracle(CasrConfig(), [12600, 11000], prec, want_lstm=40)
 
 
 @pytest.mark.parametrize("prec", PRECS)
