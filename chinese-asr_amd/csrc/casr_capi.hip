@@ -181,6 +181,7 @@ struct casr_handle {
   bool fold_ready = false;
   // (round 4) the f32 fused image: the folded greedy step under the exact-f32 arithmetic
   DevBuf wfold32;
+  DevBuf coldbuf;  // CASR_OPT_DIAG_COLD's flush source (measurement only)
   bool fold32_ready = false;
   bool s16() const { return precision == CASR_PREC_S16X3 && s16_valid; }
   int B = 0, Tp = 0;
@@ -521,7 +522,7 @@ void casr_destroy(casr_handle* h) {
   }
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->gflags, &h->fe_const,
-                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout, &h->wfold, &h->wfold32,
+                    &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout, &h->wfold, &h->wfold32, &h->coldbuf,
                     &h->egates, &h->fgates, &h->wq16})
     b->release();
   delete h;
@@ -556,12 +557,22 @@ int casr_recurrence_mode(const casr_handle* h, int B) {
 int casr_set_option(casr_handle* h, int option, int value) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
-  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0};
-  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8, 1, 1, CASR_MAX_LAYERS};
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 1, 1, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1};
   if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
     return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
   if (value < lo[option] || value > hi[option])
     return fail(h, CASR_ERR_ARG, "option %d: value %d not in [%d, %d]", option, value, lo[option], hi[option]);
+  if (option == CASR_OPT_DIAG_COLD) {
+    if (value) {
+      HIP_OK(h, hipSetDevice(h->device));
+      HIP_OK(h, h->coldbuf.ensure((size_t)1 << 30));
+      HIP_OK(h, hipMemset(h->coldbuf.p, 0, (size_t)1 << 30));
+    }
+    h->prof.cold_buf = h->coldbuf.p;
+    h->prof.cold_bytes = (size_t)1 << 30;
+    h->prof.cold_mask = (uint32_t)value;
+  }
   h->tune.v[option] = value;
   return CASR_OK;
 }

@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0, 0, 1, 0};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 1, 1, 0, 0, 1, 0, 0};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -85,8 +85,17 @@ inline int enc_gate_col(int g, int u) { return (u / 16) * 64 + (u % 16) * 4 + g;
 
 // ---------------------------------------------------------------- launch timing
 // Event pairs around launches of enabled kernel classes (casr_profile_enable).
+// flush kernel of CASR_OPT_DIAG_COLD (fill.hip): reads n float4 of buf
+hipError_t flush_caches(const void* buf, size_t bytes, hipStream_t s);
+
 struct Profiler {
   uint32_t mask = 0;
+  uint32_t cold_mask = 0;         // CASR_OPT_DIAG_COLD: classes launched after a cache flush
+  const void* cold_buf = nullptr;  // the flush kernel's 1 GiB source
+  size_t cold_bytes = 0;
+  void cold(int cls, hipStream_t s) const {
+    if (((cold_mask >> cls) & 1u) && cold_buf) (void)flush_caches(cold_buf, cold_bytes, s);
+  }
   std::vector<hipEvent_t> ev[CASR_K_COUNT];
   std::vector<int> weight[CASR_K_COUNT];  // launches covered by each event pair
   size_t used[CASR_K_COUNT] = {};
@@ -120,7 +129,10 @@ struct ProfScope {
   int cls;
   hipStream_t s;
   ProfScope(Profiler* p_, int c, hipStream_t s_, int n = 1) : p(p_), cls(c), s(s_) {
-    if (p) p->mark(cls, s, n);
+    if (p) {
+      p->cold(cls, s);  // CASR_OPT_DIAG_COLD (measurement only): before the class's first event
+      p->mark(cls, s, n);
+    }
   }
   ~ProfScope() {
     if (p) p->mark(cls, s);

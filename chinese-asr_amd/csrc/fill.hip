@@ -79,4 +79,22 @@ hipError_t copy_multi(const CopyList& cl, hipStream_t s) {
   return hipGetLastError();
 }
 
+// CASR_OPT_DIAG_COLD: stream a buffer larger than every cache level through the L2s, so the next
+// launch finds neither its L2 lines nor its Infinity-Cache lines (a sum no input can make equal
+// to the sentinel keeps the loads live; nothing is ever stored)
+__global__ void flush_caches_kernel(const float4* __restrict__ p, size_t n, float* __restrict__ never) {
+  float acc = 0.f;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float4 v = p[i];
+    acc += v.x + v.y + v.z + v.w;
+  }
+  if (acc == 1234567.f && never) never[0] = acc;
+}
+
+hipError_t flush_caches(const void* buf, size_t bytes, hipStream_t s) {
+  hipLaunchKernelGGL(flush_caches_kernel, dim3(4096), dim3(256), 0, s, reinterpret_cast<const float4*>(buf),
+                     bytes / 16, nullptr);
+  return hipGetLastError();
+}
+
 }  // namespace casr

@@ -260,7 +260,14 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            of encoder layer n - 1 as refused (hipErrorCooperativeLaunchTooLarge,
  *                            without launching), so the mid-encode fallback to the per-step
  *                            recurrence (that layer and every later one) can be checked bit for bit
- *                            against all-persistent and all-per-step encodes */
+ *                            against all-persistent and all-per-step encodes
+ * And one for measurement only (speed, never bits):
+ *   CASR_OPT_DIAG_COLD       0 (default): off; a mask of kernel classes (bit CASR_K_*): before every
+ *                            launch of such a class, a flush kernel reads a 1 GiB handle-owned buffer
+ *                            (evicting every L2 and the 256 MiB Infinity Cache), outside the class's
+ *                            timing events, so the class's time is that of cold operands: warm minus
+ *                            cold shows how much of its traffic the Infinity Cache serves
+ *                            (the GPU exposes no Infinity-Cache counter) */
 enum {
   CASR_OPT_FUSE_SELECT = 0,
   CASR_OPT_REC_LAYOUT = 1,
@@ -274,7 +281,8 @@ enum {
   CASR_OPT_ATTN_DIRECT = 9,
   CASR_OPT_DEC_FOLD = 10,
   CASR_OPT_REC_COOP_REFUSE = 11,
-  CASR_OPT_COUNT = 12
+  CASR_OPT_DIAG_COLD = 12,
+  CASR_OPT_COUNT = 13
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

@@ -14,8 +14,9 @@
 #                    CASR_OPTS value in AB_OPTS (';'-separated; "-" = defaults) -> $OUT/ab_<i>_<r>.json
 #   counters         rocprofv3 -L (the counters this box can collect) -> $OUT/counters.txt
 #   pmc              PMC passes of tools/probes/one_step.py (PMC_MODES: greedy and/or beam) with the
-#                    counter sets in PMC_SETS (';'-separated passes); ordinary recurrence launch
-#                    (REC_COOP=0, DESIGN 3.2: a cooperative launch ends in SIGSEGV under rocprofv3)
+#                    counter sets in PMC_SETS (';'-separated passes) into $OUT/pmc<PMC_TAG>_<mode>;
+#                    CASR_OPTS=$PMC_OPTS (default REC_COOP=0, the ordinary recurrence launch: DESIGN
+#                    3.2, a cooperative launch ends in SIGSEGV under rocprofv3)
 #   trace            tools/rec_trace.py
 #   prof             rocprofv3 kernel trace + stats of bench.py (greedy only) on the shipped
 #                    cooperative launch; its exit status is recorded (must be the LAST stage)
@@ -66,11 +67,11 @@ for s in $STAGES; do
     pmc)
       IFS=';' read -r -a sets <<< "${PMC_SETS:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE;FETCH_SIZE;WRITE_SIZE}"
       for mode in ${PMC_MODES:-greedy beam}; do
-        P=$OUT/pmc_$mode
+        P=$OUT/pmc${PMC_TAG}_$mode
         mkdir -p $P
         if [ $mode = beam ]; then export BEAM=8 B=256; else unset BEAM; export B=256; fi
         for i in "${!sets[@]}"; do
-          CASR_OPTS=REC_COOP=0 timeout -s KILL 120 rocprofv3 --pmc ${sets[$i]} --output-format csv -d $P/p$i -o p$i -- \
+          CASR_OPTS=${PMC_OPTS:-REC_COOP=0} timeout -s KILL 120 rocprofv3 --pmc ${sets[$i]} --output-format csv -d $P/p$i -o p$i -- \
             python3 tools/probes/one_step.py > $P/p$i.log 2>&1
           rc=$?; stop_on $rc "pmc $mode ${sets[$i]}" $P/p$i.log
         done
