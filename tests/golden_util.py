@@ -69,6 +69,37 @@ def near_tie_beam_check(tokens, score, gold, atol, rescore=None, atol_same=None,
             assert abs(rescore(b, list(tokens[b])) - score[b]) <= atol_same, b
 
 
+def records_match_up_to_rank_ties(mine, gold, atol):
+    """Finished-hypothesis records (step, then rank order: parse_finished_tensors, model.py:708-733)
+    equal up to the order of equal-scored records within one step.  Each step must record the same
+    hypotheses (token lists) with scores within ``atol``; two records of one step may appear in the
+    other order only when their scores differ by at most ``atol``, since which of two candidates
+    torch.topk ranks first (model.py:855) is then a matter of f32 summation order (measured: two
+    EOS candidates of one step 4e-6 apart swapped between the product's s16x3 and the oracle,
+    tools/probes/beam_tie_probe.py).  Returns True, or False when the lists differ otherwise."""
+    def by_step(recs):
+        out = {}
+        for t, s in recs:
+            out.setdefault(len(t), []).append((tuple(t), float(s)))
+        return out
+    a, b = by_step(mine), by_step(gold)
+    if sorted(a) != sorted(b):
+        return False
+    for l in a:
+        ra, rb = a[l], b[l]
+        if sorted(t for t, _ in ra) != sorted(t for t, _ in rb) or len(set(t for t, _ in ra)) != len(ra):
+            return False
+        sb = dict(rb)
+        if any(abs(s - sb[t]) > atol for t, s in ra):
+            return False
+        pos = {t: i for i, (t, _) in enumerate(rb)}
+        for i in range(len(ra)):
+            for j in range(i + 1, len(ra)):
+                if pos[ra[i][0]] > pos[ra[j][0]] and abs(ra[i][1] - ra[j][1]) > atol:
+                    return False
+    return True
+
+
 def near_tie_records_check(mine, gold, atol, rescore=None):
     """Finished-hypothesis records of one utterance (parse_finished_tensors order: step, then
     rank; each (tokens, score)) against the oracle's.  Returns True when the lists are identical
