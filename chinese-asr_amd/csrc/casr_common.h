@@ -88,6 +88,16 @@ CASR_DEV void lds_dma16(const float* src, float* lds_wave_base) {
                : "memory");
 }
 
+// the same DMA from a scalar base + per-lane 32-bit byte offset (global_load_lds_dwordx4 v, s[]),
+// M0 = the wave's LDS destination byte address (a 32-bit LDS offset computed by the caller)
+CASR_DEV void lds_dma16_s(uint32_t voff, const float* sbase, uint32_t lds_byte) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+               : "memory");
+}
+
 CASR_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 // Accurate variants used on every parity-relevant path (torch CPU uses libm-accurate

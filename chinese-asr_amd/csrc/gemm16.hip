@@ -365,6 +365,262 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
   }
 }
 
+// ---- ping-pong form (round 5, CASR_OPT_GEMM16_PERSIST = 2): the persistent kernel's compute loop
+// ran at ~2.3 us per 32-deep stage against ~1.5 us of MFMA (every wave of the CU
+// read its fragments after the same barrier, then multiplied, so the SIMD's MFMA pipe idled through
+// the LDS round trips).  Here the two wave groups (wm = 0: waves 0-3, wm = 1: waves 4-7; one wave of
+// each per SIMD) run one barrier apart: each 16-deep stage is a LOAD section (the stage's 12
+// fragment reads, the DMA of the stage three ahead, lgkmcnt(0)), a barrier, an MFMA section (24
+// MFMAs), a barrier; with group 1 one barrier behind, one group's MFMA section always overlaps the
+// other group's LOAD section on the same SIMD (cdna_hip_programming.md §5, the 256² 8-phase
+// template's staggered wave groups).
+//   * Stages are 16 k deep: [A 256 rows | W 256 rows] x 64 B (16 hi | 16 lo halves of the s16 row
+//     image), a ring of four (128 KB), three stages in flight.  Chunk c (16 B) of row r sits at
+//     c ^ ((r >> 2) & 3): conflict-free ds_read_b128 of 16 consecutive rows.
+//   * Hazards, by barrier count (E_i = the i-th barrier release of a tile; group 0 enters its LOAD_j
+//     after E_{2j-1}, group 1 after E_{2j}):
+//       RAW: every wave waits (counted vmcnt) for its DMA of stage j + 1 before E_{2j+1}: group 0 after
+//       MFMA_j, group 1 at the end of LOAD_j; group 0 reads stage j + 1 after E_{2j+1}.
+//       WAR: fragment reads are retired (lgkmcnt(0)) before each LOAD's closing barrier, so the
+//       stage j - 1 buffer is free after E_{2j-1}; the DMA of stage j + 3 goes into it in LOAD_j.
+//   * Epilogue per tile: the groups realign (group 0's extra barrier), each wave writes its 128 x 64
+//     accumulator slab through a private 4 KB region of the buffer of the tile's last stage (16 rows
+//     at a time, no block barrier), adds the bias (DMA'd with the tile's first stage) and stores float4
+//     rows with buffer stores, whose out-of-range rows the hardware drops (so every wave always
+//     issues 32 stores and the vmcnt counts stay exact); one barrier, then the next tile's region.
+// Arithmetic: per accumulator the same MFMAs in the same k order as gemm16_persist_kernel (16-deep
+// stage j = k-step j & 1 of 32-deep tile j >> 1), so the outputs are bitwise equal.
+constexpr int PP_ROWF = 16;                  // floats per staged row (64 B)
+constexpr int PP_OP = G16_M * PP_ROWF;       // floats per operand and stage (16 KB)
+constexpr int PP_STAGE = 2 * PP_OP;          // [A | W]
+constexpr int PP_NBUF = 4;
+constexpr int PP_LDS = PP_NBUF * PP_STAGE + 2 * G16_N;  // ring + two bias slots
+constexpr int PP_EPI_STORES = 32;            // buffer stores per wave and tile
+static_assert(PP_LDS * 4 <= 160 * 1024, "ring + bias slots fit the LDS");
+static_assert(8 * 16 * 64 <= PP_STAGE, "eight private 16 x 64 epilogue slabs fit one stage buffer");
+
+// s_waitcnt vmcnt(N) for the largest N of {40, 9, 8, 4, 0} not above `younger` (the VMEM operations
+// this wave issued after the ones to retire): a smaller N only waits for more
+CASR_DEV void pp_vm_wait(int younger) {
+  if (younger >= 40) g16_vm_wait<40>();
+  else if (younger >= 9) g16_vm_wait<9>();
+  else if (younger >= 8) g16_vm_wait<8>();
+  else if (younger >= 4) g16_vm_wait<4>();
+  else g16_vm_wait<0>();
+}
+
+// DIAG (tools/probes/gemm16_pp_probe.hip only; results then wrong): 1 = no k-loop DMA, 2 = no MFMA,
+// 4 = no epilogue stores, 8 = DMA from 1 KB contiguous sources (the same bytes in whole lines),
+// 16 = s_memtime stamps of workgroup 0's second tile (g_pp_trace: results unchanged), 32 = no
+// w_hi 2^11 multiply (the VALU of a pre-scaled W image).  PRIO: 0 no s_setprio, 1 prio 1 around each
+// MFMA section, 2 prio 1 for the later group throughout
+__device__ unsigned long long g_pp_trace[8][64][4];
+CASR_DEV unsigned long long pp_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+template <int DIAG = 0, int PRIO = 1, int SG = 0>
+__global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
+                                                           const float* __restrict__ bias, float* __restrict__ Cout,
+                                                           int M, int N, int Kp, Order16 order, int total, int nk) {
+  __shared__ __attribute__((aligned(16))) float lds[PP_LDS];
+  constexpr int NT = 2;  // 32-column MFMA tiles per wave (wave tile 128 x 64)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;  // the wave's 128-row half and 64-column quarter
+  // stagger group (SG: diagnostic alternatives of which waves run one barrier behind)
+  const int grp = SG == 0 ? wave >> 2 : SG == 1 ? wave & 1 : (wave >> 1) & 1;
+  const int r32 = lane & 31, hsel = lane >> 5;
+  const int G = gridDim.x;
+  float* const bias_lds = lds + PP_NBUF * PP_STAGE;
+
+  auto next_tile = [&](int L, int& n, int& m) {
+    while (L < total && !order.tile(L, n, m)) L += G;
+    return L;
+  };
+  // DMA of 16-deep stage s of tile (n, m) into ring buffer b: this wave's 32 A rows and 32 W rows
+  // (two 16-row instructions each), plus, with the tile's first stage, the tile's bias (every wave
+  // copies the same 1 KB into the slot, so every wave issues the same count).  Issued with a scalar
+  // base (the operand's tile rows + the stage's k offset) and per-lane 32-bit row offsets computed
+  // once per tile, so a stage's DMA costs no VALU work beside the partner's MFMAs
+  const uint32_t lds_u32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
+  uint32_t vw[2];
+  int coff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 32 + i * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+    coff[i] = (c >> 1) * 16 + (c & 1) * 4;
+    vw[i] = (uint32_t)(row * Kp + coff[i]) * 4u;  // N % 256 == 0 (host check): no clamp
+  }
+  auto a_offsets = [&](int m, uint32_t (&va)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wave * 32 + i * 16 + (lane >> 2);
+      va[i] = (uint32_t)(min(row, M - 1 - m * G16_M) * Kp + coff[i]) * 4u;
+    }
+  };
+  auto stage_dma = [&](int b, int n, int m, int s, int tpar, const uint32_t (&va)[2]) {
+    const int kb = (s >> 1) * 32 + (s & 1) * 8;  // float offset of this stage's hi piece in the row image
+    const float* sa = A16 + (size_t)m * G16_M * Kp + kb;
+    const float* sw = W16 + (size_t)n * G16_N * Kp + kb;
+    const uint32_t l0 = lds_u32 + (uint32_t)(b * PP_STAGE + wave * 32 * PP_ROWF) * 4u;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if constexpr ((DIAG & 8) != 0) {  // diagnostic: 1 KB contiguous sources (wrong data, same bytes)
+        lds_dma16_s((uint32_t)(min(wave * 32 + i * 16, M - 16 - m * G16_M) * Kp * 4 + lane * 16), A16 + (size_t)m * G16_M * Kp + (s & 15) * 16,
+                    l0 + i * 16 * PP_ROWF * 4u);
+        lds_dma16_s((uint32_t)((wave * 32 + i * 16) * Kp * 4 + lane * 16), W16 + (size_t)n * G16_N * Kp + (s & 15) * 16,
+                    l0 + (PP_OP + i * 16 * PP_ROWF) * 4u);
+      } else {
+        lds_dma16_s(va[i], sa, l0 + i * 16 * PP_ROWF * 4u);
+        lds_dma16_s(vw[i], sw, l0 + (PP_OP + i * 16 * PP_ROWF) * 4u);
+      }
+    }
+    if (s == 0)
+      lds_dma16_s((uint32_t)min(lane * 16, (N - n * G16_N - 4) * 4), bias + n * G16_N,
+                  lds_u32 + (uint32_t)(PP_NBUF * PP_STAGE + tpar * G16_N) * 4u);
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  int n, m;
+  int L = next_tile(blockIdx.x, n, m);
+  if (L >= total) return;
+  int n2 = n, m2 = m;
+  int L2 = next_tile(L + G, n2, m2);
+  int gb = 0, tpar = 0;  // ring buffer of the tile's stage 0; the tile's bias slot
+  uint32_t va[2], va2[2];  // A row offsets of this tile and of the next
+  a_offsets(m, va);
+  a_offsets(m2, va2);
+  if (PRIO == 2 && grp == 1) __builtin_amdgcn_s_setprio(1);  // static priority for the later group
+  // prologue: stages 0..2 of the first tile
+  for (int s = 0; s < 3 && s < nk; ++s) stage_dma(s, n, m, s, 0, va);
+  pp_vm_wait(nk >= 3 ? 8 : 0);  // stage 0 (and its bias) landed: younger = stages 1 and 2
+  barrier();
+  bool after_epi = false;
+  int tiles_done = 0;
+  const _Float16 two11 = (_Float16)2048.0f;
+  f32x16 acc[4][NT];
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][t][e] = 0.f;
+    // stage s of the current tile (s >= nk: of the next one) exists / carries a bias DMA
+    auto ex = [&](int s) { return s < nk || L2 < total; };
+    auto ops = [&](int s) { return ex(s) ? 4 + (s == nk ? 1 : 0) : 0; };
+    if (grp == 1) barrier();  // the stagger: group 1 runs one barrier behind group 0
+    const bool trace = (DIAG & 16) && blockIdx.x == 0 && tiles_done == 1 && lane == 0;
+    for (int j = 0; j < nk; ++j) {
+      const float* buf = lds + ((gb + j) & 3) * PP_STAGE;
+      if (trace && j < 64) g_pp_trace[wave][j][0] = pp_stamp();
+      // ---- LOAD_j: fragments of stage j, DMA of stage j + 3
+      f16x8 wh[NT], wl[NT], ah[4], al[4];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int row = wn * 64 + t * 32 + r32, sw = (row >> 2) & 3;
+        wh[t] = *reinterpret_cast<const f16x8*>(buf + PP_OP + row * PP_ROWF + ((hsel ^ sw) << 2));
+        wl[t] = *reinterpret_cast<const f16x8*>(buf + PP_OP + row * PP_ROWF + (((2 + hsel) ^ sw) << 2));
+      }
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) {
+        const int row = wm * 128 + tm * 32 + r32, sw = (row >> 2) & 3;
+        ah[tm] = *reinterpret_cast<const f16x8*>(buf + row * PP_ROWF + ((hsel ^ sw) << 2));
+        al[tm] = *reinterpret_cast<const f16x8*>(buf + row * PP_ROWF + (((2 + hsel) ^ sw) << 2));
+      }
+      const int s3 = j + 3;
+      if (!(DIAG & 1)) {
+        if (s3 < nk) stage_dma((gb + s3) & 3, n, m, s3, tpar, va);
+        else if (L2 < total) stage_dma((gb + s3) & 3, n2, m2, s3 - nk, tpar ^ 1, va2);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      f16x8 w1[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) w1[t] = (DIAG & 32) ? wh[t] : wh[t] * two11;
+      // VMEM operations issued after this wave's DMA of stage j + 1: stages j + 2, j + 3 and, while
+      // stages 1 and 2 of a tile wait, the previous tile's 32 epilogue stores
+      const int younger = (DIAG & 1) ? 0 : ops(j + 2) + ops(j + 3) + (after_epi && j < 2 ? PP_EPI_STORES : 0);
+      if (grp == 1 && j + 1 < nk) pp_vm_wait(younger);
+      barrier();
+      if (trace && j < 64) g_pp_trace[wave][j][1] = pp_stamp();
+      // ---- MFMA_j
+      if (PRIO == 1) __builtin_amdgcn_s_setprio(1);
+      if (!(DIAG & 2)) {
+#pragma unroll
+        for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], w1[t], acc[tm][t], 0, 0, 0);
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], wl[t], acc[tm][t], 0, 0, 0);
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[tm], wh[t], acc[tm][t], 0, 0, 0);
+          }
+      } else {
+        if (ah[0][0] == (_Float16)1234.f && wh[0][0] == (_Float16)4321.f) acc[0][0][0] += 1.f;
+      }
+      if (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+      if (trace && j < 64) g_pp_trace[wave][j][2] = pp_stamp();
+      if (grp == 0 && j + 1 < nk) pp_vm_wait(younger);
+      barrier();
+      if (trace && j < 64) g_pp_trace[wave][j][3] = pp_stamp();
+    }
+    if (grp == 0) barrier();  // realign the groups: every wave has passed every read of this tile
+    // ---- epilogue: per wave, 8 rounds of 16 rows x 64 columns through a private 4 KB slab
+    {
+      float* slab = lds + ((gb + nk - 1) & 3) * PP_STAGE + wave * 16 * 64;
+      const int c4 = lane & 15, rq = lane >> 4;
+      const float4 b4 = *reinterpret_cast<const float4*>(bias_lds + tpar * G16_N + wn * 64 + c4 * 4);
+      const int m0 = m * G16_M;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          Cout + (size_t)m0 * N, 0, (int)((size_t)min(G16_M, M - m0) * N * 4), 0x00020000);
+      const int cbase = n * G16_N + wn * 64 + c4 * 4;
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int e = 8 * hh; e < 8 * hh + 8; ++e)
+              slab[((e & 3) + 8 * ((e >> 2) & 1) + 4 * hsel) * 64 + t * 32 + r32] = acc[tm][t][e] * S16_LO_INV;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = rq + 4 * i;
+            const float4 v = *reinterpret_cast<const float4*>(slab + row * 64 + c4 * 4);
+            const int lr = wm * 128 + tm * 32 + 16 * hh + row;  // row within the tile
+            const float4 o = make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
+            if (!(DIAG & 4))
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, (lr * N + cbase) * 4, 0, 0);
+            else if (v.x == 12345.f)
+              Cout[0] = o.x;
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    }
+    if (L2 >= total) break;
+    // the next tile's stage 0 (+ bias) landed: younger = its stages 1, 2 and the 32 stores
+    pp_vm_wait((DIAG & 1) ? 0 : ops(nk + 1) + ops(nk + 2) + ((DIAG & 4) ? 0 : PP_EPI_STORES));
+    barrier();  // ... visible to every wave; every wave is done with its epilogue slab
+    gb = (gb + nk) & 3;
+    L = L2;
+    n = n2;
+    m = m2;
+    tpar ^= 1;
+    after_epi = !(DIAG & 4);
+    ++tiles_done;
+    L2 = next_tile(L + G, n2, m2);
+    va[0] = va2[0];
+    va[1] = va2[1];
+    a_offsets(m2, va2);
+  }
+}
 
 }  // namespace
 
@@ -403,8 +659,14 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     const Order16 om{NB, NMm, NG};
     const int total = om.blocks();
     const int Mm = std::min(M, NMm * G16_M);
-    hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
-                       N, Kp, om, total, nk);
+    if (persist == 2) {  // ping-pong form: 16-deep stages
+      const int nk16 = (K > 0 && K <= Kp ? K + 15 : Kp) / 16;
+      hipLaunchKernelGGL((gemm16_pp_kernel<0, 1>), dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
+                         N, Kp, om, total, nk16);
+    } else {
+      hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
+                         N, Kp, om, total, nk);
+    }
     if (NMm < NM) {
       const size_t r0 = (size_t)NMm * G16_M;
       const int Mt = M - (int)r0, NMt = (Mt + 127) / 128;

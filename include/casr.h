@@ -227,7 +227,9 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            cannot be co-resident fails at launch (the encode then falls back to
  *                            the per-step recurrence) instead of spinning into the hand-off timeout;
  *                            0: ordinary launch after the occupancy check
- *   CASR_OPT_GEMM16_PERSIST  1: persistent s16x3 input-projection kernel (default); 0: per tile
+ *   CASR_OPT_GEMM16_PERSIST  s16x3 input-projection kernel: 2 persistent ping-pong form (default: two
+ *                            wave groups one barrier apart, 16-deep stages on a ring of four); 1
+ *                            persistent, 32-deep stages on two buffers; 0 one workgroup per tile
  *   CASR_OPT_GEMM16_TAIL     1: the persistent kernel takes whole rounds of tiles, the rows after
  *                            them go to one launch of half tiles (default); 0: partial last round
  *   CASR_OPT_ATTN_KPB        beam rows per attention block at k > 2: 0 auto (8 at B >= 256 and

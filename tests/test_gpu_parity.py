@@ -686,7 +686,10 @@ def test_input_gemm_tail_split_bitwise(eng, B):
     """s16x3 input projection: the persistent kernel over whole rounds plus the 128 x 256 half-tile
     launch for the rows after them (default), the persistent kernel alone (CASR_OPT_GEMM16_TAIL = 0)
     and the per-tile kernel (CASR_OPT_GEMM16_PERSIST = 0) give bitwise-identical encoder outputs
-    (B = 256 and 128: 80 / 40 tiles past the last whole round; B = 37: 48 tiles in one partial round)."""
+    (B = 256 and 128: 80 / 40 tiles past the last whole round; B = 37: 48 tiles in one partial round).
+    Round 5: the ping-pong persistent kernel (CASR_OPT_GEMM16_PERSIST = 2, the default: 16-deep
+    stages, two staggered wave groups, buffer stores that drop rows past M) with and without the
+    tail split, against the round-2 persistent kernel and the per-tile kernel."""
     if eng.precision() != "s16x3":
         pytest.skip("the split-f16 input GEMM only")
     bind(eng, "peaked")
@@ -695,7 +698,7 @@ def test_input_gemm_tail_split_bitwise(eng, B):
     fb, fr = batch_fbank(frames, eng.device)
     outs = []
     try:
-        for tail, persist in ((1, 1), (0, 1), (1, 0)):
+        for tail, persist in ((1, 2), (0, 2), (1, 1), (0, 1), (1, 0)):
             eng.set_option("GEMM16_TAIL", tail)
             eng.set_option("GEMM16_PERSIST", persist)
             eng.encode_fbank(fb, fr)
@@ -703,7 +706,7 @@ def test_input_gemm_tail_split_bitwise(eng, B):
             outs.append([t.cpu() for t in eng.encoder_results()])
     finally:
         eng.set_option("GEMM16_TAIL", 1)
-        eng.set_option("GEMM16_PERSIST", 1)
+        eng.set_option("GEMM16_PERSIST", 2)
     for got in outs[1:]:
         for a, b in zip(outs[0], got):
             assert torch.equal(a, b)

@@ -1,0 +1,197 @@
+// Standalone timing, bitwise check and race screen of the ping-pong s16x3 input-projection kernel
+// (gemm16.hip gemm16_pp_kernel) against the persistent kernel, at the bench shape (M = 256 x 266,
+// N = 2048, Kp = 768 (K = 720) / 512) and at ragged M.  Diagnostic only.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I../../include -I../../chinese-asr_amd/csrc \
+//         gemm16_pp_probe.hip -o gemm16_pp_probe && ./gemm16_pp_probe [reps]
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../chinese-asr_amd/csrc/gemm16.hip"
+using namespace casr;
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+static uint16_t f2h(float x) {
+  _Float16 h = (_Float16)x;
+  uint16_t u;
+  memcpy(&u, &h, 2);
+  return u;
+}
+
+static void make_image(std::vector<uint16_t>& img, int rows, int Kp, int K, unsigned seed, float scale) {
+  img.assign((size_t)rows * Kp * 2, 0);
+  unsigned s = seed;
+  auto rnd = [&] {
+    s = s * 1664525u + 1013904223u;
+    return ((s >> 8) & 0xFFFF) / 32768.0f - 1.0f;
+  };
+  for (int r = 0; r < rows; ++r)
+    for (int k = 0; k < K; ++k) {
+      const float x = rnd() * scale;
+      const _Float16 hi = (_Float16)x;
+      const float lo = (x - (float)hi) * 2048.0f;
+      uint16_t* t = img.data() + ((size_t)r * Kp + (k / 32) * 32) * 2;
+      t[k % 32] = f2h(x);
+      t[32 + k % 32] = f2h(lo);
+    }
+}
+
+static int ncu() {
+  int v = 0;
+  CK(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0));
+  return v;
+}
+
+template <class Kern>
+static void run(Kern k, int grid, const float* A, const float* W, const float* B, float* C, int M, int N, int Kp,
+                Order16 o, int nk) {
+  hipLaunchKernelGGL(k, dim3(grid), dim3(512), 0, 0, A, W, B, C, M, N, Kp, o, o.blocks(), nk);
+}
+
+// which SIMD each wave of a 512-thread workgroup runs on (HW_REG_HW_ID: wave_id [3:0], simd_id [5:4])
+__global__ __launch_bounds__(512) void hwid_kernel(uint32_t* out) {
+  __shared__ float pad[40000];  // one workgroup per CU, as the GEMM
+  pad[threadIdx.x] = 0.f;
+  if ((threadIdx.x & 63) == 0) out[blockIdx.x * 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  if (pad[threadIdx.x] != 0.f) out[0] = 1;
+}
+
+int main(int argc, char** argv) {
+  {
+    uint32_t* d;
+    CK(hipMalloc(&d, 64 * 8 * 4));
+    hipLaunchKernelGGL(hwid_kernel, dim3(64), dim3(512), 0, 0, d);
+    std::vector<uint32_t> h(64 * 8);
+    CK(hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+    for (int b = 0; b < 4; ++b) {
+      printf("block %d simd of waves 0..7:", b);
+      for (int w = 0; w < 8; ++w) printf(" %u", (h[b * 8 + w] >> 4) & 3);
+      printf("   (cu %u)\n", (h[b * 8] >> 8) & 15);
+    }
+    CK(hipFree(d));
+  }
+  const int reps = argc > 1 ? atoi(argv[1]) : 3;
+  const int N = 2048, G = ncu();
+  for (int Kp : {768, 512}) {
+    const int K = Kp == 768 ? 720 : 512;
+    for (int M : {256 * 266, 37 * 266 + 5}) {
+      std::vector<uint16_t> a, w;
+      make_image(a, M, Kp, K, 1u + M, 3.0f);
+      make_image(w, N, Kp, K, 2u, 0.05f);
+      std::vector<float> bias(N);
+      for (int i = 0; i < N; ++i) bias[i] = 0.001f * (i % 97) - 0.05f;
+      float *dA, *dW, *dB, *dC0, *dC1;
+      CK(hipMalloc(&dA, a.size() * 2));
+      CK(hipMalloc(&dW, w.size() * 2));
+      CK(hipMalloc(&dB, N * 4));
+      CK(hipMalloc(&dC0, (size_t)M * N * 4 + 4096));
+      CK(hipMalloc(&dC1, (size_t)M * N * 4 + 4096));
+      CK(hipMemcpy(dA, a.data(), a.size() * 2, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dW, w.data(), w.size() * 2, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dB, bias.data(), N * 4, hipMemcpyHostToDevice));
+      const int NB = N / G16_N, NM = (M + G16_M - 1) / G16_M;
+      int NG = 1;
+      while (NG < 8 && NB % (NG * 2) == 0 && (size_t)(NB / NG) * G16_N * Kp * 4 > (3u << 20)) NG *= 2;
+      const Order16 o{NB, NM, NG};
+      const int nk32 = (K + 31) / 32, nk16 = (K + 15) / 16;
+      const int grid = std::min(o.blocks(), G);
+      // reference: the persistent kernel
+      CK(hipMemset(dC0, 0, (size_t)M * N * 4 + 4096));
+      run(gemm16_persist_kernel<0>, grid, dA, dW, dB, dC0, M, N, Kp, o, nk32);
+      CK(hipDeviceSynchronize());
+      std::vector<float> c0((size_t)M * N + 1024), c1((size_t)M * N + 1024);
+      CK(hipMemcpy(c0.data(), dC0, c0.size() * 4, hipMemcpyDeviceToHost));
+      // race screen: pp output bitwise equal on every rep (the guard words past M x N untouched)
+      size_t bad = 0;
+      for (int r = 0; r < reps; ++r) {
+        CK(hipMemset(dC1, 0xFF, (size_t)M * N * 4 + 4096));
+        run(gemm16_pp_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(c1.data(), dC1, c1.size() * 4, hipMemcpyDeviceToHost));
+        size_t diff = 0;
+        for (size_t i = 0; i < (size_t)M * N; ++i)
+          if (memcmp(&c0[i], &c1[i], 4) != 0) {
+            if (diff < 3) printf("  rep %d diff at row %zu col %zu: %g vs %g\n", r, i / N, i % N, c0[i], c1[i]);
+            ++diff;
+          }
+        for (size_t i = (size_t)M * N; i < c1.size(); ++i)
+          if (__builtin_bit_cast(uint32_t, c1[i]) != 0xFFFFFFFFu) ++diff;
+        bad += diff;
+      }
+      printf("Kp %d M %d: pp vs persist: %zu differing outputs over %d reps\n", Kp, M, bad, reps);
+      if (M == 256 * 266) {
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        // per-stage timeline of workgroup 0's second tile (s_memtime stamps, DIAG 16; the same results)
+        for (int dg : {16, 17}) {
+          if (dg == 16) run(gemm16_pp_kernel<16, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+          else run(gemm16_pp_kernel<21, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+          CK(hipDeviceSynchronize());
+          unsigned long long tr[8][64][4];
+          CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_pp_trace), sizeof tr));
+          printf("trace %s (cycles from wave 0's first stamp): per stage j, wave: load->A, A->mfma end, ->B\n",
+                 dg == 16 ? "full" : "mfma+lds");
+          const unsigned long long t0 = tr[0][0][0];
+          for (int j = 0; j < 12; ++j) {
+            printf("  j %2d:", j);
+            for (int w : {0, 4})
+              printf("  w%d @%6lld load %4lld mfma %4lld waitB %4lld |", w, (long long)(tr[w][j][0] - t0),
+                     (long long)(tr[w][j][1] - tr[w][j][0]), (long long)(tr[w][j][2] - tr[w][j][1]),
+                     (long long)(tr[w][j][3] - tr[w][j][2]));
+            printf("\n");
+          }
+          double per = (double)(tr[0][31][0] - tr[0][1][0]) / 30.0;
+          printf("  average stage period (w0, stages 1..31): %.0f cycles\n", per);
+        }
+        const char* names[] = {"persist", "pp", "pp:no-dma", "pp:no-mfma", "pp:no-stores", "pp:contig",
+                               "pp:contig-no-mfma", "pp:dma-only", "pp:mfma+lds", "pp:lds-only", "pp:prio0",
+                               "pp:prio2", "pp:noscale", "pp:prio0-noscale", "pp:prio0 mfma+lds"};
+        for (int rep = 0; rep < 3; ++rep)
+          for (int v = 0; v < 15; ++v) {
+            const int iters = 10;
+            CK(hipEventRecord(e0));
+            for (int i = 0; i < iters; ++i) {
+              if (v == 0) run(gemm16_persist_kernel<0>, grid, dA, dW, dB, dC0, M, N, Kp, o, nk32);
+              else if (v == 1) run(gemm16_pp_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 2) run(gemm16_pp_kernel<1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 3) run(gemm16_pp_kernel<2>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 4) run(gemm16_pp_kernel<4>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 5) run(gemm16_pp_kernel<8>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 6) run(gemm16_pp_kernel<10>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 7) run(gemm16_pp_kernel<6>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 8) run(gemm16_pp_kernel<5>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 9) run(gemm16_pp_kernel<7>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 10) run(gemm16_pp_kernel<0, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 11) run(gemm16_pp_kernel<0, 2>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 12) run(gemm16_pp_kernel<32, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 13) run(gemm16_pp_kernel<32, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else run(gemm16_pp_kernel<5, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+            }
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const double flop = 2.0 * M * N * (double)(16 * nk16) * 3;
+            printf("Kp %d %-14s %8.1f us  %6.0f TF/s f16 (K used %d)\n", Kp, names[v], 1000.0 * ms / iters,
+                   flop / (ms / iters * 1e-3) / 1e12, 16 * nk16);
+          }
+      }
+      CK(hipFree(dA));
+      CK(hipFree(dW));
+      CK(hipFree(dB));
+      CK(hipFree(dC0));
+      CK(hipFree(dC1));
+    }
+  }
+  return 0;
+}
