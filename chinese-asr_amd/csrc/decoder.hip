@@ -242,7 +242,10 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
         else seg = k0 < ASrc::kSeg ? aseg[j][0] + k0 : aseg[j][NSEG - 1] + (k0 - ASrc::kSeg);
         if constexpr (B32) {
           const int row = 8 * i + (lane >> 3), p = (lane & 7) ^ (row & 7);
-          lds_dma16(seg + 16 * (p >> 1) + 8 * (kt & 1) + 4 * (p & 1), la + i * 256);
+          if constexpr ((CASR_DG_DIAG & 128) != 0)  // diagnostic: the stage's 128 B of a row contiguous (wrong data)
+            lds_dma16(seg + 32 * (kt & 1) + 4 * p, la + i * 256);
+          else
+            lds_dma16(seg + 16 * (p >> 1) + 8 * (kt & 1) + 4 * (p & 1), la + i * 256);
         } else {
           const int row = 4 * i + (lane >> 4), c = (lane & 15) ^ (row & 15);
           lds_dma16(seg + c * 4, la + i * 256);

@@ -422,11 +422,14 @@ CASR_DEV unsigned long long pp_stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
-template <int DIAG = 0, int PRIO = 1, int SG = 0>
+template <int DIAG = 0, int PRIO = 1, int SG = 0, int AGPR = 0>
 __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
                                                            const float* __restrict__ bias, float* __restrict__ Cout,
                                                            int M, int N, int Kp, Order16 order, int total, int nk) {
   __shared__ __attribute__((aligned(16))) float lds[PP_LDS];
+  // AGPR: an AGPR clobber keeps the accumulation registers available, so hipcc picks the MFMA form
+  // with the accumulators in AGPRs (C / D traffic off the VGPR file the partner's LDS returns use)
+  if constexpr (AGPR != 0) asm volatile("; accumulators in AGPRs" ::: "a0");
   constexpr int NT = 2;  // 32-column MFMA tiles per wave (wave tile 128 x 64)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;  // the wave's 128-row half and 64-column quarter

@@ -114,7 +114,8 @@ int main(int argc, char** argv) {
       size_t bad = 0;
       for (int r = 0; r < reps; ++r) {
         CK(hipMemset(dC1, 0xFF, (size_t)M * N * 4 + 4096));
-        run(gemm16_pp_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+        if (r & 1) run(gemm16_pp_kernel<0, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+        else run(gemm16_pp_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(c1.data(), dC1, c1.size() * 4, hipMemcpyDeviceToHost));
         size_t diff = 0;
@@ -134,8 +135,8 @@ int main(int argc, char** argv) {
         CK(hipEventCreate(&e1));
         // per-stage timeline of workgroup 0's second tile (s_memtime stamps, DIAG 16; the same results)
         for (int dg : {16, 17}) {
-          if (dg == 16) run(gemm16_pp_kernel<16, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-          else run(gemm16_pp_kernel<21, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+          if (dg == 16) run(gemm16_pp_kernel<16, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+          else run(gemm16_pp_kernel<21, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
           CK(hipDeviceSynchronize());
           unsigned long long tr[8][64][4];
           CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_pp_trace), sizeof tr));
@@ -155,7 +156,7 @@ int main(int argc, char** argv) {
         }
         const char* names[] = {"persist", "pp", "pp:no-dma", "pp:no-mfma", "pp:no-stores", "pp:contig",
                                "pp:contig-no-mfma", "pp:dma-only", "pp:mfma+lds", "pp:lds-only", "pp:prio0",
-                               "pp:prio2", "pp:noscale", "pp:prio0-noscale", "pp:prio0 mfma+lds"};
+                               "pp:prio2", "pp:agpr", "pp:agpr-prio0", "pp:agpr mfma+lds"};
         for (int rep = 0; rep < 3; ++rep)
           for (int v = 0; v < 15; ++v) {
             const int iters = 10;
@@ -173,9 +174,9 @@ int main(int argc, char** argv) {
               else if (v == 9) run(gemm16_pp_kernel<7>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
               else if (v == 10) run(gemm16_pp_kernel<0, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
               else if (v == 11) run(gemm16_pp_kernel<0, 2>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 12) run(gemm16_pp_kernel<32, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 13) run(gemm16_pp_kernel<32, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else run(gemm16_pp_kernel<5, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 12) run(gemm16_pp_kernel<0, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 13) run(gemm16_pp_kernel<0, 0, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else run(gemm16_pp_kernel<5, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
             }
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
