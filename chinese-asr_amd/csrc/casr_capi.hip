@@ -557,8 +557,8 @@ int casr_recurrence_mode(const casr_handle* h, int B) {
 int casr_set_option(casr_handle* h, int option, int value) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
-  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0};
-  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 2, 1, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1};
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 2, 1, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1, 1};
   if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
     return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
   if (value < lo[option] || value > hi[option])
@@ -625,7 +625,7 @@ int casr_log_mel(casr_handle* h, const float* wav, const int32_t* n_samples, int
   if (!guard_words(h)) return fail(h, CASR_ERR_HIP, "casr_log_mel: guard words not allocated");
   ProfScope ps(&h->prof, CASR_K_FEATURES, s);
   HIP_OK(h, launch_log_mel(wav, n_samples, B, n_max, t_max, preemphasis, h->fe_const.as<FrontendConst>(), fbank,
-                           frames, GUARD(h, 2), s));
+                           frames, GUARD(h, 2), s, h->tune[CASR_OPT_LOGMEL_Q16]));
   return CASR_OK;
 }
 

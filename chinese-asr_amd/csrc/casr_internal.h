@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 1, 0, 0, 1, 0, 0};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 1, 0, 0, 1, 0, 0, 1};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -213,8 +213,10 @@ struct FrontendConst {
 void mel_filterbank(int n_stft, float f_min, float f_max, int n_mels, float* fb);
 void build_frontend_const(FrontendConst* c);
 int frontend_frames(int n_samples);
+// form: 1 = the 16-lane kernel (default), 0 = one wave per frame (round 4); the same bits
 hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nmax, int Tmax, float pre,
-                          const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s);
+                          const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s,
+                          int form = 1);
 
 // features.hip
 // the layer-0 s16 row image straight from fbank (features_rows_kernel<true>, T <= 1024)

@@ -35,17 +35,15 @@ constexpr int NC = NFFT / 2;  // complex FFT size
 constexpr int FE_WAVES = 4;   // waves (frames in flight) per block
 constexpr int FE_FPW = 8;     // consecutive frames per wave
 constexpr int FE_W0 = 10, FE_W1 = 17;  // widest of mel filters 0..63 / 64..79 (build_frontend_const checks)
+#ifndef FQ_FPQ
+#define FQ_FPQ 4  // frames per quad (log_mel_q16_kernel)
+#endif
 
 // torch's elementwise steps, each rounded (no FMA contraction: hipcc's default would fuse them):
-// pre-emphasis x[t+1] - 0.97 x[t] (data.py:201-202), the window product, |X|^2 = re^2 + im^2
-// (data.py:220-221)
+// pre-emphasis x[t+1] - 0.97 x[t] (data.py:201-202), the window product (|X|^2: split_power)
 CASR_DEV float preemph_win(float w, float x1, float x0, float pre) {
 #pragma clang fp contract(off)
   return w * (x1 - pre * x0);
-}
-CASR_DEV float power2(float re, float im) {
-#pragma clang fp contract(off)
-  return re * re + im * im;
 }
 
 // exchange slot of FFT position p (conflict-free for the four stage patterns)
@@ -54,7 +52,24 @@ CASR_DEV int fe_slot(int p) { return p ^ ((p >> 2) & 31); }
 CASR_DEV int rev4(int k) {
   return ((k & 3) << 6) | (((k >> 2) & 3) << 4) | (((k >> 4) & 3) << 2) | ((k >> 6) & 3);
 }
-CASR_DEV float2 cmul(float2 a, float2 w) { return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x); }
+// complex product with its contraction written out (both log-mel kernels: the same bits whatever
+// code surrounds it; hipcc's default contraction of a.x w.x - a.y w.y depends on the context)
+CASR_DEV float2 cmul(float2 a, float2 w) {
+#pragma clang fp contract(off)
+  const float p = a.y * w.y, q = a.y * w.x;
+  return make_float2(fmaf(a.x, w.x, -p), fmaf(a.x, w.y, q));
+}
+
+// the real-input split of bin q and its power: X[q] = E + W512^q O, E = (Z[q] + conj Z[-q]) / 2,
+// O = (Z[q] - conj Z[-q]) / 2i, P = |X[q]|^2 (data.py:220-221), contraction written out
+CASR_DEV float split_power(float2 z1, float2 z2, float2 tq) {
+#pragma clang fp contract(off)
+  const float er = 0.5f * (z1.x + z2.x), ei = 0.5f * (z1.y - z2.y);
+  const float orr = 0.5f * (z1.y + z2.y), oi = -0.5f * (z1.x - z2.x);
+  const float xr = er + fmaf(orr, tq.x, -(oi * tq.y));
+  const float xi = ei + fmaf(orr, tq.y, oi * tq.x);
+  return xr * xr + xi * xi;
+}
 
 // one radix-4 DIF butterfly: y_q = sum_r a_r (-i)^(rq), then y_q *= w_q (q = 1..3)
 CASR_DEV void bfly4(float2 (&a)[4], const float2 (&w)[3], bool twiddle) {
@@ -200,11 +215,7 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
       const int q = lane + 64 * r;
       if (q < NBIN) {
         const float2 z1 = zs[w][fe_slot(rev4(q & (NC - 1)))], z2 = zs[w][fe_slot(rev4((NC - q) & (NC - 1)))];
-        const float er = 0.5f * (z1.x + z2.x), ei = 0.5f * (z1.y - z2.y);
-        const float orr = 0.5f * (z1.y + z2.y), oi = -0.5f * (z1.x - z2.x);
-        const float2 tq = t512s[q];
-        const float c = tq.x, sn = tq.y;
-        pw[w][q] = power2(er + (orr * c - oi * sn), ei + (orr * sn + oi * c));
+        pw[w][q] = split_power(z1, z2, t512s[q]);
       }
     }
     lds_fence();
@@ -230,6 +241,168 @@ __global__ __launch_bounds__(256) void log_mel_kernel(const float* __restrict__ 
     mel(std::integral_constant<int, FE_W0>{}, lane, fw0);
     if (lane + 64 < F) mel(std::integral_constant<int, FE_W1>{}, lane + 64, fw1);
     lds_fence();  // this frame's pw / zs reads are done before the next frame's writes
+  }
+}
+
+// ---- the 16-lane form (round 5, the default): 16 lanes per frame, 16 points per lane, 4 frames per
+// wave in flight.  With lane l holding the points m = l + 16 r (r = 0..15), the butterflies of
+// radix-4 DIF stages 0 (stride 64) and 1 (stride 16) are all within the lane; one transpose through
+// LDS gives lane l the points 16 l + i, and stages 2 (stride 4) and 3 (stride 1) are again within the
+// lane.  So a frame is one stage exchange instead of three (log_mel_kernel: six dependent LDS round
+// trips per frame), with the same butterflies, twiddles and operation order: the same bits as
+// log_mel_kernel (tests/test_gpu_frontend.py).  Exchange slot p ^ ((p >> 4) & 15): the transpose's
+// writes (p = l + 16 r) and reads (p = 16 l + i) of a quad are conflict-free; quads are 128 B apart.
+// Lane l's constants for every frame: the stage-0 and stage-1 twiddles and the weights of its mel
+// filters l + 16 i (i < 4: filters 0..63, at most FE_W0 bins; i = 4: 64..79, at most FE_W1).
+constexpr int FQ_Q = 8;   // frames in flight per block: 2 waves x 4 quads of 16 lanes
+constexpr int FQ_ZS = NC + 16;  // float2 per quad's exchange buffer (+128 B: quads apart in the banks)
+CASR_DEV int fq_slot(int p) { return p ^ ((p >> 4) & 15); }
+
+template <int FPQ>
+__global__ __launch_bounds__(64 * FQ_Q / 4) void log_mel_q16_kernel(const float* __restrict__ wav,
+                                                                    const int32_t* __restrict__ nsamp, int Nmax,
+                                                                    int Tmax, float pre,
+                                                                    const FrontendConst* __restrict__ k,
+                                                                    float* __restrict__ out,
+                                                                    int32_t* __restrict__ frames,
+                                                                    int32_t* __restrict__ err) {
+  __shared__ float2 zs[FQ_Q][FQ_ZS];
+  __shared__ float pw[FQ_Q][NBIN + 3];
+  __shared__ float2 wins[NC];  // (w[2m], w[2m + 1]) of point m
+  __shared__ float2 t256[NC], t512s[NBIN];
+  __shared__ float fbs[F][FE_W1 + 1];  // the filters' weights (+1: the 16 lanes' rows in distinct banks)
+  __shared__ int lohi[F];
+  const int b = blockIdx.y, tid = threadIdx.x, qd = tid >> 4, l = tid & 15;
+  for (int i = tid; i < NC; i += blockDim.x) {
+    t256[i] = make_float2(k->tw256r[i], k->tw256i[i]);
+    const int j0 = 2 * i - LPAD, j1 = j0 + 1;
+    wins[i] = make_float2(j0 >= 0 && j0 < WIN ? k->win[j0] : 0.f, j1 >= 0 && j1 < WIN ? k->win[j1] : 0.f);
+  }
+  for (int i = tid; i < NBIN; i += blockDim.x) t512s[i] = make_float2(k->tw512r[i], k->tw512i[i]);
+  for (int i = tid; i < F * FE_W1; i += blockDim.x) fbs[i / FE_W1][i % FE_W1] = k->fb[i / FE_W1][i % FE_W1];
+  for (int i = tid; i < F; i += blockDim.x) lohi[i] = k->lo[i];
+  __syncthreads();  // the only block barrier: the quads run their frames independently after it
+  int n = nsamp[b];
+  if (n < NFFT + 1 || n > Nmax) {
+    if (blockIdx.x == 0 && tid == 0) atomicOr(err, CASR_DEV_BAD_AUDIO);
+    n = n > Nmax ? Nmax : n;
+  }
+  const int L = n - 1 >= NFFT ? 1 + (n - 1 - NFFT) / HOP : 0;  // frames of the pre-emphasised signal
+  if (blockIdx.x == 0 && tid == 0) frames[b] = L < Tmax ? L : Tmax;
+  const int f0 = (blockIdx.x * FQ_Q + qd) * FPQ;
+  float2* z = zs[qd];
+  float* p = pw[qd];
+  // the samples of a frame: point m = l + 16 r needs x[2m .. 2m + 2] (x[512] at most: inside the
+  // signal for every frame f < L); loaded one frame ahead, so a frame's loads fly while the previous
+  // frame computes.  All points are loaded, from one lane pointer with immediate offsets: the window
+  // zeroes the ones outside it, as the reference's full-frame product does
+  float xs[16][3];
+  auto load_frame = [&](int f) {
+    const bool live = f < L && f < Tmax;
+    const float* x = wav + (size_t)b * Nmax + (size_t)(live ? f : 0) * HOP + 2 * l;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) xs[r][e] = x[32 * r + e];
+  };
+  load_frame(f0);
+  for (int fi = 0; fi < FPQ; ++fi) {
+    const int f = f0 + fi;
+    if (f >= Tmax) break;
+    float* o = out + ((size_t)b * Tmax + f) * F;
+    if (f >= L) {  // padding rows past the utterance (quad-uniform)
+#pragma unroll
+      for (int i = 0; i < 5; ++i) o[l + 16 * i] = 0.f;
+      continue;
+    }
+    float2 a[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {  // point m = l + 16 r: (y[2m] w[2m], y[2m+1] w[2m+1])
+      const float2 wv = wins[l + 16 * r];
+      a[r] = make_float2(preemph_win(wv.x, xs[r][1], xs[r][0], pre), preemph_win(wv.y, xs[r][2], xs[r][1], pre));
+    }
+    if (fi + 1 < FPQ) load_frame(f + 1);
+    // stage 0 (stride 64): group r' = points l + 16 r' + 64 q = a[r' + 4 q], twiddle j = l + 16 r'
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float2 tw[3];
+#pragma unroll
+      for (int q = 1; q <= 3; ++q) tw[q - 1] = t256[((l + 16 * r) * q) & (NC - 1)];
+      float2 g[4] = {a[r], a[r + 4], a[r + 8], a[r + 12]};
+      bfly4(g, tw, true);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[r + 4 * q] = g[q];
+    }
+    // stage 1 (stride 16): group g = points 64 g + l + 16 q = a[4 g + q], twiddle j = l
+    {
+      float2 tw[3];
+#pragma unroll
+      for (int q = 1; q <= 3; ++q) tw[q - 1] = t256[(4 * l * q) & (NC - 1)];
+#pragma unroll
+      for (int gi = 0; gi < 4; ++gi) {
+        float2 g[4] = {a[4 * gi], a[4 * gi + 1], a[4 * gi + 2], a[4 * gi + 3]};
+        bfly4(g, tw, true);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[4 * gi + q] = g[q];
+      }
+    }
+    // the transpose: lane l takes the points 16 l + i
+#pragma unroll
+    for (int r = 0; r < 16; ++r) z[fq_slot(l + 16 * r)] = a[r];
+    lds_fence();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = z[fq_slot(16 * l + i)];
+    // stage 2 (stride 4): group o = points 16 l + o + 4 q = a[o + 4 q], twiddle j = o
+#pragma unroll
+    for (int oo = 0; oo < 4; ++oo) {
+      float2 tw[3];
+#pragma unroll
+      for (int q = 1; q <= 3; ++q) tw[q - 1] = t256[(16 * oo * q) & (NC - 1)];
+      float2 g[4] = {a[oo], a[oo + 4], a[oo + 8], a[oo + 12]};
+      bfly4(g, tw, true);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[oo + 4 * q] = g[q];
+    }
+    // stage 3 (stride 1): group = points 16 l + 4 gi + q = a[4 gi + q], no twiddle
+#pragma unroll
+    for (int gi = 0; gi < 4; ++gi) {
+      float2 g[4] = {a[4 * gi], a[4 * gi + 1], a[4 * gi + 2], a[4 * gi + 3]};
+      const float2 tw[3] = {};
+      bfly4(g, tw, false);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[4 * gi + q] = g[q];
+    }
+    lds_fence();  // the transpose's reads are done before the spectrum overwrites the buffer
+    // Z[k] sits at position rev4(k) = 16 l + i
+#pragma unroll
+    for (int i = 0; i < 16; ++i) z[fq_slot(16 * l + i)] = a[i];
+    lds_fence();
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {  // bins q = l + 16 i (and 256 on lane 0)
+      const int q = l + 16 * i;
+      if (q < NBIN) p[q] = split_power(z[fq_slot(rev4(q & (NC - 1)))], z[fq_slot(rev4((NC - q) & (NC - 1)))], t512s[q]);
+    }
+    lds_fence();
+    // mel projection: a float32 fma chain over the filter's bins in bin order (fixed trip counts,
+    // zero weights past its last bin), then log with the FLT_EPSILON floor (data.py:222-224)
+    auto mel = [&](auto NW, int m) {
+      constexpr int W = decltype(NW)::value;
+      const int lo = lohi[m];
+      float pv[W], wv[W];
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        pv[i] = p[min(lo + i, NBIN - 1)];
+        wv[i] = fbs[m][i];
+      }
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < W; ++i) acc = fmaf(pv[i], wv[i], acc);  // matmul: fused
+      o[m] = logf(acc == 0.f ? 1.1920928955078125e-07f : acc);
+    };
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mel(std::integral_constant<int, FE_W0>{}, l + 16 * i);
+    mel(std::integral_constant<int, FE_W1>{}, 64 + l);
+    lds_fence();  // this frame's pw / z reads are done before the next frame's writes
   }
 }
 }  // namespace
@@ -297,10 +470,18 @@ int frontend_frames(int n_samples) {
 }
 
 hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nmax, int Tmax, float pre,
-                          const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s) {
-  constexpr int FPB = FE_WAVES * FE_FPW;  // frames per block
-  dim3 grid((Tmax + FPB - 1) / FPB > 0 ? (Tmax + FPB - 1) / FPB : 1, B);
-  hipLaunchKernelGGL(log_mel_kernel<>, grid, dim3(256), 0, s, wav, nsamp, Nmax, Tmax, pre, k, out, frames, err);
+                          const FrontendConst* k, float* out, int32_t* frames, int32_t* err, hipStream_t s,
+                          int form) {
+  if (form == 0) {  // the one-wave-per-frame form (round 4), kept for comparison: the same bits
+    constexpr int FPB = FE_WAVES * FE_FPW;  // frames per block
+    dim3 grid((Tmax + FPB - 1) / FPB > 0 ? (Tmax + FPB - 1) / FPB : 1, B);
+    hipLaunchKernelGGL(log_mel_kernel<>, grid, dim3(256), 0, s, wav, nsamp, Nmax, Tmax, pre, k, out, frames, err);
+  } else {
+    constexpr int FPB = FQ_Q * FQ_FPQ;
+    dim3 grid((Tmax + FPB - 1) / FPB > 0 ? (Tmax + FPB - 1) / FPB : 1, B);
+    hipLaunchKernelGGL(log_mel_q16_kernel<FQ_FPQ>, grid, dim3(16 * FQ_Q), 0, s, wav, nsamp, Nmax, Tmax, pre, k, out,
+                       frames, err);
+  }
   return hipGetLastError();
 }
 

@@ -232,6 +232,9 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            persistent, 32-deep stages on two buffers; 0 one workgroup per tile
  *   CASR_OPT_GEMM16_TAIL     1: the persistent kernel takes whole rounds of tiles, the rows after
  *                            them go to one launch of half tiles (default); 0: partial last round
+ *   CASR_OPT_LOGMEL_Q16      1: casr_log_mel runs 16 lanes per frame, 16 FFT points per lane, one
+ *                            stage exchange per frame (default, round 5); 0: one wave per frame, three
+ *                            stage exchanges (round 4).  The same butterflies in the same order
  *   CASR_OPT_ATTN_KPB        beam rows per attention block at k > 2: 0 auto (8 at B >= 256 and
  *                            k >= 8, else 4), 4 or 8
  * Two options select numerics variants instead (the same token ids, floating-point results within
@@ -284,7 +287,8 @@ enum {
   CASR_OPT_DEC_FOLD = 10,
   CASR_OPT_REC_COOP_REFUSE = 11,
   CASR_OPT_DIAG_COLD = 12,
-  CASR_OPT_COUNT = 13
+  CASR_OPT_LOGMEL_Q16 = 13,
+  CASR_OPT_COUNT = 14
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

@@ -53,8 +53,8 @@ static int ncu() {
 
 template <class Kern>
 static void run(Kern k, int grid, const float* A, const float* W, const float* B, float* C, int M, int N, int Kp,
-                Order16 o, int nk) {
-  hipLaunchKernelGGL(k, dim3(grid), dim3(512), 0, 0, A, W, B, C, M, N, Kp, o, o.blocks(), nk);
+                Order16 o, int nk, int threads = 512) {
+  hipLaunchKernelGGL(k, dim3(grid), dim3(threads), 0, 0, A, W, B, C, M, N, Kp, o, o.blocks(), nk);
 }
 
 // which SIMD each wave of a 512-thread workgroup runs on (HW_REG_HW_ID: wave_id [3:0], simd_id [5:4])
@@ -114,8 +114,8 @@ int main(int argc, char** argv) {
       size_t bad = 0;
       for (int r = 0; r < reps; ++r) {
         CK(hipMemset(dC1, 0xFF, (size_t)M * N * 4 + 4096));
-        if (r & 1) run(gemm16_pp_kernel<0, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-        else run(gemm16_pp_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+        if (r & 1) run(gemm16_pp_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+        else run(gemm16_w4_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(c1.data(), dC1, c1.size() * 4, hipMemcpyDeviceToHost));
         size_t diff = 0;
@@ -128,35 +128,14 @@ int main(int argc, char** argv) {
           if (__builtin_bit_cast(uint32_t, c1[i]) != 0xFFFFFFFFu) ++diff;
         bad += diff;
       }
-      printf("Kp %d M %d: pp vs persist: %zu differing outputs over %d reps\n", Kp, M, bad, reps);
+      printf("Kp %d M %d: w4 (even reps) / pp (odd) vs persist: %zu differing outputs over %d reps\n", Kp, M, bad, reps);
       if (M == 256 * 266) {
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
-        // per-stage timeline of workgroup 0's second tile (s_memtime stamps, DIAG 16; the same results)
-        for (int dg : {16, 17}) {
-          if (dg == 16) run(gemm16_pp_kernel<16, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-          else run(gemm16_pp_kernel<21, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-          CK(hipDeviceSynchronize());
-          unsigned long long tr[8][64][4];
-          CK(hipMemcpyFromSymbol(tr, HIP_SYMBOL(g_pp_trace), sizeof tr));
-          printf("trace %s (cycles from wave 0's first stamp): per stage j, wave: load->A, A->mfma end, ->B\n",
-                 dg == 16 ? "full" : "mfma+lds");
-          const unsigned long long t0 = tr[0][0][0];
-          for (int j = 0; j < 12; ++j) {
-            printf("  j %2d:", j);
-            for (int w : {0, 4})
-              printf("  w%d @%6lld load %4lld mfma %4lld waitB %4lld |", w, (long long)(tr[w][j][0] - t0),
-                     (long long)(tr[w][j][1] - tr[w][j][0]), (long long)(tr[w][j][2] - tr[w][j][1]),
-                     (long long)(tr[w][j][3] - tr[w][j][2]));
-            printf("\n");
-          }
-          double per = (double)(tr[0][31][0] - tr[0][1][0]) / 30.0;
-          printf("  average stage period (w0, stages 1..31): %.0f cycles\n", per);
-        }
         const char* names[] = {"persist", "pp", "pp:no-dma", "pp:no-mfma", "pp:no-stores", "pp:contig",
-                               "pp:contig-no-mfma", "pp:dma-only", "pp:mfma+lds", "pp:lds-only", "pp:prio0",
-                               "pp:prio2", "pp:agpr", "pp:agpr-prio0", "pp:agpr mfma+lds"};
+                               "pp:contig-no-mfma", "pp:dma-only", "pp:mfma+lds", "pp:lds-only", "w4",
+                               "w4:no-dma", "w4:no-mfma", "w4:no-stores", "w4:mfma+lds"};
         for (int rep = 0; rep < 3; ++rep)
           for (int v = 0; v < 15; ++v) {
             const int iters = 10;
@@ -172,11 +151,11 @@ int main(int argc, char** argv) {
               else if (v == 7) run(gemm16_pp_kernel<6>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
               else if (v == 8) run(gemm16_pp_kernel<5>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
               else if (v == 9) run(gemm16_pp_kernel<7>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 10) run(gemm16_pp_kernel<0, 0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 11) run(gemm16_pp_kernel<0, 2>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 12) run(gemm16_pp_kernel<0, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 13) run(gemm16_pp_kernel<0, 0, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else run(gemm16_pp_kernel<5, 1, 0, 1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 10) run(gemm16_w4_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
+              else if (v == 11) run(gemm16_w4_kernel<1>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
+              else if (v == 12) run(gemm16_w4_kernel<2>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
+              else if (v == 13) run(gemm16_w4_kernel<4>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
+              else run(gemm16_w4_kernel<5>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
             }
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
