@@ -64,6 +64,36 @@ def test_log_mel_ragged_batch_matches_oracle(eng):
         assert (fb[b, ref.shape[0]:] == 0).all()
 
 
+@pytest.mark.parametrize("golden", [True, False])
+def test_log_mel_forms_bitwise_equal(eng, golden):
+    """CASR_OPT_LOGMEL_Q16 (round 5): the 16-lanes-per-frame kernel (default: radix-4 stages 0-1 and
+    2-3 in registers around one transpose) and the one-wave-per-frame kernel (three stage exchanges)
+    run the same butterflies with the same twiddles in the same order, so their log-mel outputs are
+    bitwise equal: on the reference's wav0 and on a ragged batch (padding frames, a silent stretch,
+    the shortest valid signal of 513 samples)."""
+    if golden:
+        ns = [G["wav0"].shape[0]]
+        wav = G["wav0"][None].astype(np.float32)
+    else:
+        ns = [513, 673, 16000, 24000, 47999, 5000, 800, 128353]
+        wav = np.zeros((len(ns), max(ns)), np.float32)
+        for b, n in enumerate(ns):
+            wav[b, :n] = synth_wav(n, 300 + b)
+        wav[4, 9000:9800] = 0.0
+    w = torch.from_numpy(wav).cuda()
+    outs = []
+    try:
+        for form in (1, 0):
+            eng.set_option("LOGMEL_Q16", form)
+            fb, frames = eng.log_mel(w, torch.tensor(ns, dtype=torch.int32))
+            assert eng.device_flags() == 0
+            outs.append((fb.cpu(), frames.cpu()))
+    finally:
+        eng.set_option("LOGMEL_Q16", 1)
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][0], outs[1][0])
+
+
 def test_log_mel_short_audio_flag(eng):
     wav = torch.from_numpy(synth_wav(2000, 5)[None].repeat(2, 0)).cuda()
     fb, frames = eng.log_mel(wav, torch.tensor([2000, 400], dtype=torch.int32))

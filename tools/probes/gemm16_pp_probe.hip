@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../chinese-asr_amd/csrc/gemm16.hip"
+#include "gemm16_w4.hip"
 using namespace casr;
 
 #define CK(x)                                                                  \
