@@ -16,6 +16,7 @@
 
 #include <type_traits>
 
+#include "beam_select.h"
 #include "casr_common.h"
 #include "casr_internal.h"
 
@@ -107,7 +108,9 @@ __device__ uint32_t* g_at_trace = nullptr;
 // its rows on gates_prev + emb_gates[tok] and q = h . W_hidden itself (no query partials); st
 // receives h, c (and ctx as always).  CELL 1, greedy (KPB = 1, row r = b): the block first runs the
 // select of step l - 1 for its row.  CELL 2, beam (KPB = 4 or 8): tokens and predecessor rows come
-// from the beam select; gates_prev and c are read at the predecessor row.
+// from the beam select; gates_prev and c are read at the predecessor row.  CELL 3, beam with one
+// block per utterance (KPB = k = 4 or 8): the block first runs the beam select of step l - 1 for
+// its utterance (beam_select.h) and takes the tokens and predecessor rows from it.
 template <int KPB, int CELL = 0>
 __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float* __restrict__ st, const float* __restrict__ qpart, const float* __restrict__ keysT,
@@ -116,14 +119,17 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     int l, int total, int npf, int direct, int nq, int V, AttnCell cell) {
   static_assert(CELL != 1 || KPB == 1, "the folded greedy step: one row per block");
   static_assert(CELL != 2 || KPB >= 2, "the folded beam step: beam rows of one utterance per block");
+  static_assert(CELL != 3 || KPB == 4 || KPB == 8, "the fused beam select: one block per utterance, k = 4 or 8");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   uint32_t* atr = g_at_trace ? g_at_trace + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int i) {
     if (atr && threadIdx.x == 0) atr[i] = (uint32_t)__builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  // (CELL: the early exit is decided after the block's own select, below)
-  if (CELL != 1 && done_before(newdone, l) >= total) return;
+  // (CELL 1: the early exit is decided after the block's own select, below.  CELL 3: the select of
+  // step l - 1 skips when every utterance finished before step l - 1; otherwise the block runs it and
+  // the attention, whatever this launch's selects add to step l - 1's count)
+  if (CELL != 1 && done_before(newdone, CELL == 3 ? l - 1 : l) >= total) return;
   const int Tq = attn_tq(Tp);
   float* qs = sm;                   // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
   float* eqs = qs + KPB * AT_APAD;  // [AT_APAD][KPB]: exp(2q) (split form), zero past A
@@ -151,7 +157,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   constexpr int CH = KPB >= 8 ? AT_CH / 2 : AT_CH;  // KPB 8: half the keys rows per batch (registers)
   // CELL: the first keys batch of this thread's first score item (split form) is loaded before the
   // cell phase, which it does not depend on, so the scores start on landed keys
-  constexpr bool PRE = CELL == 1 || (CELL == 2 && KPB >= 8);  // (KPB 4: 20 keys rows per batch, no registers left)
+  constexpr bool PRE = CELL == 1 || (CELL >= 2 && KPB >= 8);  // (KPB 4: 20 keys rows per batch, no registers left)
   float4 kvp[PRE ? CH : 1];
   // CELL 1, 2 (round 4): unconditional loads at clamped addresses, masked at use.  Per-slot
   // conditional loads compile to lane-masked regions, and their joins made hipcc wait for every load
@@ -326,7 +332,24 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       eqs[a] = split_exp2x(q);
     }
   }
-  if constexpr (CELL == 2) {
+  if constexpr (CELL >= 2) {
+    // (CELL 3) the beam select of step l - 1 for utterance b, in the score scratch (free until the
+    // scores); its tokens and predecessor rows also go to bs_tok / bs_src, prefilled with what
+    // tok / src hold, as the separate launch leaves slots no candidate fills
+    __shared__ int bs_tok[CELL == 3 ? KPB : 1], bs_src[CELL == 3 ? KPB : 1];
+    if constexpr (CELL == 3) {
+      using SelLds = BeamSelLds<2 * KPB, KPB, AT_WAVES>;
+      static_assert(sizeof(SelLds) <= attn_scratch_floats<KPB>(4) * sizeof(float), "the select's LDS fits the scratch");
+      if (tid < KPB) {
+        bs_tok[tid] = cell.bs.tok_next[row0 + tid];
+        bs_src[tid] = cell.bs.src_next[row0 + tid];
+      }
+      SelLds& sl = *reinterpret_cast<SelLds*>(xs);
+      if (cell.bs.temperature == 1.0f) beam_select_block<2 * KPB, true>(cell.bs, b, sl, nullptr, bs_tok, bs_src);
+      else beam_select_block<2 * KPB, false>(cell.bs, b, sl, nullptr, bs_tok, bs_src);
+      __syncthreads();  // bs_tok / bs_src written; the scratch is free again
+      stamp(6);
+    }
     // 0. the folded beam step's LSTM cell for the block's nk rows r = row0 + j: token tok[r],
     // predecessor s = src[r] (clamped and reported like DecLstmA::bind); thread = unit u.  Then
     // q = h . W_hidden for the block's rows as s16x3 MFMAs (the split words of h, rows padded to 16,
@@ -342,7 +365,14 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 #pragma unroll
     for (int j = 0; j < KPB; ++j) {
       const int r = (int)row0 + min(j, nk - 1);
-      int sj = cell.src[r], tj = cell.tok[r];
+      int sj, tj;
+      if constexpr (CELL == 3) {
+        sj = bs_src[min(j, nk - 1)];
+        tj = bs_tok[min(j, nk - 1)];
+      } else {
+        sj = cell.src[r];
+        tj = cell.tok[r];
+      }
       bad |= (unsigned)sj >= (unsigned)R ? CASR_DEV_BAD_SRC : 0;
       bad |= (unsigned)tj >= (unsigned)V ? CASR_DEV_BAD_TOKEN : 0;
       sr[j] = (unsigned)sj < (unsigned)R ? sj : r;
@@ -805,8 +835,12 @@ hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const Attn
                                       int32_t* newdone, int l, int total, hipStream_t s) {
   if (a.k == 1) return launch_kpb<1, 1>(a, st, nullptr, align, newdone, l, total, s, cell);
   switch (attention_kpb(a.B, a.k, a.attn_kpb)) {
-    case 4: return launch_kpb<4, 2>(a, st, nullptr, align, newdone, l, total, s, cell);
-    case 8: return launch_kpb<8, 2>(a, st, nullptr, align, newdone, l, total, s, cell);
+    case 4:
+      if (cell.bsel) return a.k == 4 ? launch_kpb<4, 3>(a, st, nullptr, align, newdone, l, total, s, cell) : hipErrorInvalidValue;
+      return launch_kpb<4, 2>(a, st, nullptr, align, newdone, l, total, s, cell);
+    case 8:
+      if (cell.bsel) return a.k == 8 ? launch_kpb<8, 3>(a, st, nullptr, align, newdone, l, total, s, cell) : hipErrorInvalidValue;
+      return launch_kpb<8, 2>(a, st, nullptr, align, newdone, l, total, s, cell);
     default: return hipErrorInvalidValue;  // the folded beam step needs 4 or 8 rows per block
   }
 }

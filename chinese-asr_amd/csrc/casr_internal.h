@@ -277,6 +277,28 @@ struct GreedyPart {
 };
 constexpr int GP_NT = 320;  // 16-column tiles per row (V <= 5120)
 
+// a beam select's operands and outputs (beam_select.h; beam_select_kernel's argument, and the
+// folded beam attention's prologue select, AttnCell::bs)
+struct BeamSelArgs {
+  const float* logits;
+  int V, B, k, l, L, eos;
+  float temperature;
+  const float* score_cur;
+  float* score_next;
+  int32_t* tok_next;
+  int32_t* src_next;
+  uint8_t* topfin;
+  int32_t* bp;
+  int32_t* tk;
+  float* rec_score;
+  int32_t* rec_src;
+  uint8_t* rec_valid;
+  int32_t* newdone;
+  int32_t* err;
+  GreedyPart gp;
+  int nbp;
+};
+
 // Greedy select of step lsel fused into a later kernel of step lsel + 1 (the LSTMCell GEMM's
 // prologue, decoder.hip DecLstmA; or the folded step's attention kernel, attention.hip): the
 // projection's per-block row partials of step lsel are reduced by the consumer itself and the
@@ -410,6 +432,8 @@ struct AttnCell {
   int32_t* err;
   int sel;
   GreedySel gs;
+  int bsel;        // beam, one block per utterance: the select of step l - 1 runs in the prologue (bs)
+  BeamSelArgs bs;
 };
 hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const AttnCell& cell, float* align,
                                       int32_t* newdone, int l, int total, hipStream_t s);

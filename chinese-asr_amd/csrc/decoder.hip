@@ -23,6 +23,7 @@
 #include <type_traits>
 #include <vector>
 
+#include "beam_select.h"
 #include "casr_common.h"
 #include "casr_internal.h"
 
@@ -1021,10 +1022,6 @@ struct ArgMax {
   float v;
   int i;
 };
-__device__ __forceinline__ bool better(float av, int ai, float bv, int bi) {
-  return av > bv || (av == bv && ai < bi);
-}
-
 __global__ __launch_bounds__(256) void greedy_select_kernel(
     const float* __restrict__ logits, int V, int R, int l, int L, int eos, int32_t* __restrict__ tok_next,
     int32_t* __restrict__ src_next, uint8_t* __restrict__ fin, int32_t* __restrict__ out_len, float* __restrict__ accum,
@@ -1163,482 +1160,15 @@ __global__ __launch_bounds__(256) void greedy_select_part_kernel(
   }
 }
 
-// ------------------------------------------------------------------ beam select
-template <int K2>
-struct TopList {
-  float v[K2];
-  int i[K2];
-  __device__ __forceinline__ void init() {
-#pragma unroll
-    for (int p = 0; p < K2; ++p) {
-      v[p] = -INFINITY;
-      i[p] = 0x7fffffff;
-    }
-  }
-  __device__ __forceinline__ void insert(float xv, int xi) {
-    if (!better(xv, xi, v[K2 - 1], i[K2 - 1])) return;
-    v[K2 - 1] = xv;
-    i[K2 - 1] = xi;
-#pragma unroll
-    for (int p = K2 - 1; p > 0; --p) {
-      if (better(v[p], i[p], v[p - 1], i[p - 1])) {
-        const float tv = v[p];
-        v[p] = v[p - 1];
-        v[p - 1] = tv;
-        const int ti = i[p];
-        i[p] = i[p - 1];
-        i[p - 1] = ti;
-      }
-    }
-  }
-  __device__ __forceinline__ void pop() {
-#pragma unroll
-    for (int p = 0; p < K2 - 1; ++p) {
-      v[p] = v[p + 1];
-      i[p] = i[p + 1];
-    }
-    v[K2 - 1] = -INFINITY;
-    i[K2 - 1] = 0x7fffffff;
-  }
-};
-
-// Extract the top n (<= K2) of the union of the 64 lanes' sorted lists; lane 0 writes them.
-template <int K2>
-__device__ __forceinline__ void wave_merge(TopList<K2>& L, int n, float* outv, int* outi) {
-  for (int c = 0; c < n; ++c) {
-    float bv = L.v[0];
-    int bi = L.i[0];
-    wave_best(bv, bi);
-    if (L.i[0] == bi && L.v[0] == bv) L.pop();
-    if ((threadIdx.x & 63) == 0) {
-      outv[c] = bv;
-      outi[c] = bi;
-    }
-  }
-}
-
-// One block per utterance, one wave per beam row (rows j = w, w + 8): three exact passes
-// over the row (max, sum of exp -> lse; then val = (x/T - lse) + score inserted into a
-// per-lane sorted list), the lane lists merged with wave shuffles to the row's top-2k, then
-// wave 0 merges the k rows' lists from LDS into the utterance's top-2k (torch.topk over
-// the k*V flattened scores, model.py:860-865; ties -> lower flat index).
-constexpr int BS_CAP = 256;  // threshold candidates kept per row (beyond: full selection)
-
-// UNIT_T: temperature == 1 (the reference default, gpd['temperature']): x / T is x exactly, so the
-// three per-element divisions of each pass are skipped (bitwise the same values)
-// 8 waves, one per beam row (k = 16: two rows each).  Measured at k = 16 (B = 128): 16 waves
-// of one row each (1024 threads, <= 128 VGPRs: the register-resident row does not fit, so they
-// take the two-pass path) 45.7 us per step against 38.7 us for 8 waves on the register path.
-template <int K2>
-constexpr int bs_waves() {
-  return 8;
-}
+// ------------------------------------------------------------------ beam select (beam_select.h)
 template <int K2, bool UNIT_T>
-__global__ __launch_bounds__(64 * bs_waves<K2>()) void beam_select_kernel(
-    const float* __restrict__ logits, int V, int B, int k, int l, int L, int eos, float temperature,
-    const float* __restrict__ score_cur, float* __restrict__ score_next,
-    int32_t* __restrict__ tok_next, int32_t* __restrict__ src_next, uint8_t* __restrict__ topfin,
-    int32_t* __restrict__ bp, int32_t* __restrict__ tk, float* __restrict__ rec_score,
-    int32_t* __restrict__ rec_src, uint8_t* __restrict__ rec_valid, int32_t* __restrict__ newdone,
-    int32_t* __restrict__ err, GreedyPart gp, int nbp) {
-  __shared__ float rv_s[KMAX_BEAM][K2];
-  __shared__ int ri_s[KMAX_BEAM][K2];
-  __shared__ float rv2_s[KMAX_BEAM / 2][K2];  // block-merge tree: the other buffer of each level
-  __shared__ int ri2_s[KMAX_BEAM / 2][K2];
-  __shared__ float cv[K2];
-  __shared__ int ci[K2];
-  constexpr int NWV = bs_waves<K2>(), NTH = 64 * NWV;
-  __shared__ float cv_s[NWV][BS_CAP];  // per-wave threshold candidates
-  __shared__ int ci_s[NWV][BS_CAP];
-  __shared__ int cnt_s[NWV];
+__global__ __launch_bounds__(64 * bs_waves<K2>()) void beam_select_kernel(BeamSelArgs a) {
+  constexpr int NWV = bs_waves<K2>();
+  __shared__ BeamSelLds<K2, KMAX_BEAM, NWV> lds;
   uint32_t* btr = g_dg_trace ? g_dg_trace + ((size_t)2 * 4096 + blockIdx.x) * 8 : nullptr;
-  auto stamp = [&](int i, uint32_t v) {
-    if (btr && threadIdx.x == 0) btr[i] = v;
-  };
-  stamp(0, (uint32_t)__builtin_amdgcn_s_memrealtime());
-  if (done_before(newdone, l) >= B) return;
-  const int b = blockIdx.x, tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
-  const int R = B * k;
-  const int nrows = (l == 0) ? 1 : k;  // model.py:862-863: step 0 ranks beam 0 only
-  const int n2k = 2 * k;
-  const bool vec = (V & 3) == 0;
-  auto xt = [&](float x) { return UNIT_T ? x : x / temperature; };
-
-  for (int j = wv; j < nrows; j += NWV) {
-    const float* x = logits + (size_t)(b * k + j) * V;
-    const float4* x4 = reinterpret_cast<const float4*>(x);
-    const float sc = score_cur[b * k + j];
-    constexpr int TPL = GP_NT / 64;  // tile maxima per lane
-    int nc;
-    float lse;  // the row's logsumexp
-    if (UNIT_T && nbp > 0 && gp.tmx && vec) {
-      // From the projection's partials: block (max, sum exp) -> logsumexp, and the maximum of
-      // every 16-column tile.  tau = the exact 2k-th largest tile maximum (in candidate value,
-      // monotone in x): the tile maxima are distinct elements, so tau bounds the row's 2k-th best
-      // value from below, and every element of the top 2k lies in a tile whose maximum is >= tau.
-      // Only those tiles (2k of them, ties aside) are read: 16 logits each instead of the row.
-      const size_t row = (size_t)(b * k + j);
-      float mb = -INFINITY, sb = 0.f;
-      if (ln < nbp) {
-        mb = gp.mx[row * GP_NB + ln];
-        sb = gp.se[row * GP_NB + ln];
-      }
-      const int ntile = (V + 15) / 16;
-      float tm[TPL];
-      int tt[TPL];
-#pragma unroll
-      for (int c = 0; c < TPL; ++c) {
-        tt[c] = ln + 64 * c;
-        tm[c] = tt[c] < ntile ? gp.tmx[row * GP_NT + tt[c]] : -INFINITY;
-      }
-      const float M = wave_max(mb);
-      const float s = wave_sum((sb > 0.f) ? sb * expf(mb - M) : 0.f);
-      lse = logf(s) + M;
-      // this lane's tiles in descending maximum (a 5-element sorting network of swaps)
-#pragma unroll
-      for (int i = 0; i < TPL; ++i)
-#pragma unroll
-        for (int c = 0; c + 1 < TPL - i; ++c)
-          if (tm[c + 1] > tm[c]) {
-            const float fv = tm[c];
-            tm[c] = tm[c + 1];
-            tm[c + 1] = fv;
-            const int iv = tt[c];
-            tt[c] = tt[c + 1];
-            tt[c + 1] = iv;
-          }
-      // each lane's best tile is read ahead, under the tau rounds (the qualifying tiles are the
-      // 2k best, most of them each the best of its lane); the rest only if they qualify.  Reading
-      // the two best ahead measured the same.
-      constexpr int PRE = 1;
-      float4 xq[TPL][4];
-#pragma unroll
-      for (int c = 0; c < PRE; ++c)
-#pragma unroll
-        for (int h = 0; h < 4; ++h) xq[c][h] = x4[min(tt[c], ntile - 1) * 4 + h];
-      if (j == 0) stamp(1, (uint32_t)__builtin_amdgcn_s_memrealtime());
-      float tau = -INFINITY;
-      {
-        float hd[TPL];  // this lane's remaining tile maxima, head first
-#pragma unroll
-        for (int c = 0; c < TPL; ++c) hd[c] = (tm[c] - lse) + sc;
-        for (int c = 0; c < n2k; ++c) {
-          const float mx = wave_max(hd[0]);
-          tau = mx;
-          const unsigned long long hit = __ballot(hd[0] == mx);
-          if (hit && ln == __ffsll((long long)hit) - 1) {
-#pragma unroll
-            for (int i = 0; i + 1 < TPL; ++i) hd[i] = hd[i + 1];
-            hd[TPL - 1] = -INFINITY;
-          }
-        }
-      }
-      // the qualifying tiles' logits (all loads issued before any use), then the candidates
-      // val >= tau compacted per wave without atomics: per-lane counts, their exclusive prefix over
-      // the wave from bit-sliced ballots (counts <= 80 < 128), each lane writing from its offset
-      bool qual[TPL];
-#pragma unroll
-      for (int c = 0; c < TPL; ++c) {
-        qual[c] = (tm[c] - lse) + sc >= tau;
-        if (c >= PRE) {
-#pragma unroll
-          for (int h = 0; h < 4; ++h)
-            xq[c][h] = qual[c] ? x4[tt[c] * 4 + h] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-        }
-      }
-      // per-slot 16-bit hit masks; a slot no lane of the wave qualifies in (the usual case past the
-      // lanes' best tiles) is skipped by a wave-uniform branch
-      uint32_t hm[TPL];
-      int cnt = 0;
-#pragma unroll
-      for (int c = 0; c < TPL; ++c) {
-        hm[c] = 0u;
-        if (__ballot(qual[c])) {
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const int n0 = tt[c] * 16 + 4 * h;
-            const float xs[4] = {xq[c][h].x, xq[c][h].y, xq[c][h].z, xq[c][h].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              hm[c] |= (qual[c] && n0 + e < V && (xs[e] - lse) + sc >= tau) ? (1u << (4 * h + e)) : 0u;
-          }
-          cnt += __popc(hm[c]);
-        }
-      }
-      const unsigned long long below = (1ull << ln) - 1ull;
-      int slot = 0, total = 0;
-#pragma unroll
-      for (int bit = 0; bit < 7; ++bit) {
-        const unsigned long long mk = __ballot((cnt >> bit) & 1);
-        slot += __popcll(mk & below) << bit;
-        total += __popcll(mk) << bit;
-      }
-#pragma unroll
-      for (int c = 0; c < TPL; ++c) {
-        if (__ballot(hm[c] != 0u)) {
-#pragma unroll
-          for (int h = 0; h < 4; ++h) {
-            const int n0 = tt[c] * 16 + 4 * h;
-            const float xs[4] = {xq[c][h].x, xq[c][h].y, xq[c][h].z, xq[c][h].w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if ((hm[c] >> (4 * h + e)) & 1u) {
-                if (slot < BS_CAP) {
-                  cv_s[wv][slot] = (xs[e] - lse) + sc;  // model.py:834-836
-                  ci_s[wv][slot] = j * V + n0 + e;
-                }
-                ++slot;
-              }
-          }
-        }
-      }
-      nc = total;
-    } else {
-    // the row read whole (temperature != 1, or a vocabulary beyond the tile-maxima table): the
-    // row's logsumexp and this lane's largest and second-largest candidate values (for tau)
-    float lt, lt2;
-    {
-      float lm = -INFINITY, lm2 = -INFINITY;  // this lane's two largest x / T (distinct elements)
-      auto top2 = [&](float y) {
-        lm2 = fmaxf(lm2, fminf(lm, y));
-        lm = fmaxf(lm, y);
-      };
-      if (vec) {
-#pragma unroll 4
-        for (int i = ln; i < V / 4; i += 64) {
-          const float4 q = x4[i];
-          top2(xt(q.x));
-          top2(xt(q.y));
-          top2(xt(q.z));
-          top2(xt(q.w));
-        }
-      } else {
-        for (int v = ln; v < V; v += 64) top2(xt(x[v]));
-      }
-      const float m = wave_max(lm);
-      float s = 0.f;
-      if (vec) {
-#pragma unroll 4
-        for (int i = ln; i < V / 4; i += 64) {
-          const float4 q = x4[i];
-          s += expf(xt(q.x) - m) + expf(xt(q.y) - m) + expf(xt(q.z) - m) + expf(xt(q.w) - m);
-        }
-      } else {
-        for (int v = ln; v < V; v += 64) s += expf(xt(x[v]) - m);
-      }
-      s = wave_sum(s);
-      lse = logf(s) + m;
-      lt = (lm - lse) + sc;
-      lt2 = (lm2 - lse) + sc;
-    }
-    if (j == 0) stamp(1, (uint32_t)__builtin_amdgcn_s_memrealtime());
-    // tau = the 2k-th largest of the lanes' candidate values: each round takes the largest and
-    // exposes that lane's next one
-    float tau = -INFINITY;
-    for (int c = 0; c < n2k; ++c) {
-      const float mx = wave_max(lt);
-      tau = mx;
-      const unsigned long long hit = __ballot(lt == mx);
-      if (hit && ln == __ffsll((long long)hit) - 1) {
-        lt = lt2;
-        lt2 = -INFINITY;
-      }
-    }
-    if (ln == 0) cnt_s[wv] = 0;
-    __builtin_amdgcn_wave_barrier();
-    auto offer = [&](float val, int idx) {
-      if (val >= tau) {
-        const int slot = atomicAdd(&cnt_s[wv], 1);
-        if (slot < BS_CAP) {
-          cv_s[wv][slot] = val;
-          ci_s[wv][slot] = idx;
-        }
-      }
-    };
-    if (vec) {
-      // all of a lane's row loads in flight at once (20 float4 cover V = 5004), not two per
-      // round trip
-      constexpr int QB = 20;
-      for (int i0 = ln; i0 < V / 4; i0 += 64 * QB) {
-        float4 q[QB];
-#pragma unroll
-        for (int u = 0; u < QB; ++u) {
-          const int i = i0 + 64 * u;
-          q[u] = i < V / 4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < QB; ++u) {
-          const int i = i0 + 64 * u;
-          if (i >= V / 4) break;
-          offer((xt(q[u].x) - lse) + sc, j * V + 4 * i);
-          offer((xt(q[u].y) - lse) + sc, j * V + 4 * i + 1);
-          offer((xt(q[u].z) - lse) + sc, j * V + 4 * i + 2);
-          offer((xt(q[u].w) - lse) + sc, j * V + 4 * i + 3);
-        }
-      }
-    } else {
-      for (int v = ln; v < V; v += 64) offer((xt(x[v]) - lse) + sc, j * V + v);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    nc = cnt_s[wv];
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's candidates are in cv_s / ci_s
-    __builtin_amdgcn_wave_barrier();
-    if (j == 0) {
-      stamp(2, (uint32_t)__builtin_amdgcn_s_memrealtime());
-      stamp(7, (uint32_t)nc);
-    }
-    if (nc <= BS_CAP) {
-      // rank selection over the row's threshold candidates (a few dozen): a candidate's slot is
-      // the number of candidates better than it (better(): value, then lower flat index; indices
-      // are distinct, so ranks are too); slots no candidate reaches keep the (-inf, INT_MAX)
-      // sentinel the sorted-list merge (wave_merge) produces for them.  Same list, in sorted
-      // order, as the per-lane insertion + wave_merge below, without its 2k shuffle rounds.
-      if (ln < n2k) {
-        rv_s[j][ln] = -INFINITY;
-        ri_s[j][ln] = 0x7fffffff;
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (nc <= 64) {  // one candidate per lane, the others read from registers (readlane)
-        const float pv = ln < nc ? cv_s[wv][ln] : -INFINITY;
-        const int pi = ln < nc ? ci_s[wv][ln] : 0x7fffffff;
-        int rank = 0;
-        for (int q = 0; q < nc; ++q)
-          rank += better(readlane_f(pv, q), __builtin_amdgcn_readlane(pi, q), pv, pi) ? 1 : 0;
-        if (ln < nc && rank < n2k) {
-          rv_s[j][rank] = pv;
-          ri_s[j][rank] = pi;
-        }
-      } else {
-        for (int p = ln; p < nc; p += 64) {
-          const float pv = cv_s[wv][p];
-          const int pi = ci_s[wv][p];
-          int rank = 0;
-          for (int q = 0; q < nc; ++q) rank += better(cv_s[wv][q], ci_s[wv][q], pv, pi) ? 1 : 0;
-          if (rank < n2k) {
-            rv_s[j][rank] = pv;
-            ri_s[j][rank] = pi;
-          }
-        }
-      }
-      if (j == 0) {
-        stamp(3, (uint32_t)__builtin_amdgcn_s_memrealtime());
-        stamp(4, (uint32_t)__builtin_amdgcn_s_memrealtime());
-      }
-    } else {  // more ties at tau than the buffer holds: every element through sorted lane lists
-      TopList<K2> tl;
-      tl.init();
-      if (vec) {
-        for (int i = ln; i < V / 4; i += 64) {
-          const float4 q = x4[i];
-          tl.insert((xt(q.x) - lse) + sc, j * V + 4 * i);  // model.py:834-836
-          tl.insert((xt(q.y) - lse) + sc, j * V + 4 * i + 1);
-          tl.insert((xt(q.z) - lse) + sc, j * V + 4 * i + 2);
-          tl.insert((xt(q.w) - lse) + sc, j * V + 4 * i + 3);
-        }
-      } else {
-        for (int v = ln; v < V; v += 64) tl.insert((xt(x[v]) - lse) + sc, j * V + v);
-      }
-      if (j == 0) stamp(3, (uint32_t)__builtin_amdgcn_s_memrealtime());
-      wave_merge<K2>(tl, n2k, rv_s[j], ri_s[j]);
-      if (j == 0) stamp(4, (uint32_t)__builtin_amdgcn_s_memrealtime());
-    }
-  }
-  __syncthreads();  // every row's sorted list is in rv_s / ri_s
-  // block merge: the rows' sorted lists are merged pairwise in a tree (nrows -> 1 in
-  // ceil(log2 nrows) levels), each level keeping the top 2k of every pair.  An entry's slot in its
-  // pair's merged list is its position in its own list + the number of entries of the other list
-  // better than it (better(): value, then lower flat index; a binary search over that sorted list),
-  // one thread per entry, every wave taking part.  Real candidates have distinct indices, so
-  // distinct slots; the (-inf, INT_MAX) sentinels that fill short lists land on slots only
-  // sentinels reach.  Same list, in the same order, as the one-wave sorted-list merge (TopList +
-  // wave_merge) this replaces.
-  {
-    float(*sv)[K2] = rv_s;
-    int(*si)[K2] = ri_s;
-    float(*dv)[K2] = rv2_s;
-    int(*di)[K2] = ri2_s;
-    int nl = nrows;
-    while (nl > 1) {
-      const int npair = nl >> 1;
-      for (int t = tid; t < npair * 2 * n2k; t += NTH) {
-        const int pr = t / (2 * n2k), side = (t / n2k) & 1, pos = t - (2 * pr + side) * n2k;
-        const float xv = sv[2 * pr + side][pos];
-        const int xi = si[2 * pr + side][pos];
-        const int o = 2 * pr + 1 - side;
-        int lo = 0, hi = n2k;  // entries of list o better than x: a prefix of it
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (better(sv[o][mid], si[o][mid], xv, xi)) lo = mid + 1;
-          else hi = mid;
-        }
-        const int slot = pos + lo;
-        if (slot < n2k) {
-          dv[pr][slot] = xv;
-          di[pr][slot] = xi;
-        }
-      }
-      if ((nl & 1) && tid < n2k) {  // an odd list out moves up unchanged
-        dv[npair][tid] = sv[nl - 1][tid];
-        di[npair][tid] = si[nl - 1][tid];
-      }
-      __syncthreads();
-      float(*tv)[K2] = sv;
-      int(*ti)[K2] = si;
-      sv = dv;
-      si = di;
-      dv = tv;
-      di = ti;
-      nl = npair + (nl & 1);
-    }
-    if (tid < n2k) {
-      cv[tid] = sv[0][tid];
-      ci[tid] = si[0][tid];
-    }
-  }
-  __syncthreads();
-  stamp(5, (uint32_t)__builtin_amdgcn_s_memrealtime());
-
-  // bookkeeping, one lane of wave 0 per ranked candidate c < 2k (the serial loops of
-  // model.py:874-909 as ballots: a non-EOS candidate's slot is its rank among the non-EOS ones,
-  // an EOS candidate's is (#non-EOS) + its rank among the EOS ones; slots >= k are dropped)
-  if (wv == 0) {
-    const int c = ln;
-    const bool inr = c < n2k;
-    int cc = inr ? ci[c] : 0;
-    const bool bad = inr && (unsigned)cc >= (unsigned)(nrows * V);  // NaN rows leave empty slots
-    if (bad) cc = 0;
-    if (__ballot(bad) && ln == 0) atomicOr(err, CASR_DEV_BAD_CAND);
-    const int beam = cc / V, tok = cc - beam * V;
-    const bool f = inr && tok == eos;
-    const float cs = inr ? cv[c] : 0.f;
-    if (c < k) {  // finished hypotheses among the first k candidates (model.py:874-889)
-      const size_t ri = ((size_t)b * L + l) * k + c;
-      rec_valid[ri] = f;
-      if (f) {
-        rec_score[ri] = cs;
-        rec_src[ri] = beam;
-      }
-    }
-    if (ln == 0 && !topfin[b] && tok == eos) {  // model.py:897-901 (candidate 0)
-      topfin[b] = 1;
-      atomicAdd(&newdone[l], 1);
-    }
-    // active = first k non-EOS candidates in rank order, then EOS ones (model.py:904-909)
-    const unsigned long long ne = __ballot(inr && !f), eo = __ballot(f);
-    const unsigned long long below = (1ull << c) - 1ull;
-    const int slot = f ? __popcll(ne) + __popcll(eo & below) : __popcll(ne & below);
-    if (inr && slot < k) {
-      const int row = b * k + slot;
-      tok_next[row] = tok;
-      src_next[row] = b * k + beam;
-      score_next[row] = cs;
-      bp[(size_t)l * R + row] = beam;
-      tk[(size_t)l * R + row] = tok;
-    }
-    stamp(6, (uint32_t)__builtin_amdgcn_s_memrealtime());
-  }
+  if (btr && threadIdx.x == 0) btr[0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  if (done_before(a.newdone, a.l) >= a.B) return;
+  beam_select_block<K2, UNIT_T>(a, blockIdx.x, lds, btr, nullptr, nullptr);
 }
 
 // executed loop steps: the step at which the cumulative count reached `total`, + 1
@@ -1949,7 +1479,7 @@ static void fold_gemm_step(const DecodeArgs& a, DecodeBufs& d, int l, int total,
 // the folded step's attention with its cell prologue (steps l >= 1): greedy with the fused select
 // of step l - 1 (sel), beam with the beam select's tokens and predecessor rows
 static hipError_t fold_attention_step(const DecodeArgs& a, DecodeBufs& d, int l, int total, float* align,
-                                      bool sel, const GreedySel& gs, hipStream_t s) {
+                                      bool sel, const GreedySel& gs, hipStream_t s, const BeamSelArgs* bs = nullptr) {
   ProfScope ps(a.prof, CASR_K_ATTENTION, s);
   AttnCell cell{};
   cell.st_old = d.st[l & 1];
@@ -1962,6 +1492,10 @@ static hipError_t fold_attention_step(const DecodeArgs& a, DecodeBufs& d, int l,
   cell.err = d.err;
   cell.sel = sel ? 1 : 0;
   cell.gs = gs;
+  if (bs) {
+    cell.bsel = 1;
+    cell.bs = *bs;
+  }
   return launch_attention_cell_step(a, d.st[(l + 1) & 1], cell, align, d.newdone, l, total, s);
 }
 
@@ -2032,13 +1566,19 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
   return hipGetLastError();
 }
 
+// the select of step l: logits and partials of step l's GEMM, scores of step l in, step l + 1's
+// tokens / predecessors / scores out
+static BeamSelArgs beam_sel_args(const DecodeArgs& a, const DecodeBufs& d, int l) {
+  return BeamSelArgs{d.logits, a.V, a.B, a.k, l, a.max_len, a.eos, a.temperature, d.score[l & 1],
+                     d.score[(l + 1) & 1], d.tok[(l + 1) & 1], d.src[(l + 1) & 1], d.topfin, d.bp, d.tk,
+                     d.rec_score, d.rec_src, d.rec_valid, d.newdone, d.err, d.part,
+                     row_partials(a) ? proj_col_blocks(a) : 0};
+}
+
 template <int K2>
 static void launch_beam_select(const DecodeArgs& a, DecodeBufs& d, int l, hipStream_t s) {
   auto kern = a.temperature == 1.0f ? beam_select_kernel<K2, true> : beam_select_kernel<K2, false>;
-  hipLaunchKernelGGL(kern, dim3(a.B), dim3(64 * bs_waves<K2>()), 0, s, d.logits, a.V, a.B, a.k, l,
-                     a.max_len, a.eos, a.temperature, d.score[l & 1], d.score[(l + 1) & 1],
-                     d.tok[(l + 1) & 1], d.src[(l + 1) & 1], d.topfin, d.bp, d.tk, d.rec_score,
-                     d.rec_src, d.rec_valid, d.newdone, d.err, d.part, row_partials(a) ? proj_col_blocks(a) : 0);
+  hipLaunchKernelGGL(kern, dim3(a.B), dim3(64 * bs_waves<K2>()), 0, s, beam_sel_args(a, d, l));
 }
 
 hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float length_weight,
@@ -2052,15 +1592,25 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
   if (e0 != hipSuccess) return e0;
   hipLaunchKernelGGL(decode_init_kernel, dim3(R), dim3(256), 0, s, d.st[0], a.hfin, a.cfin, a.B, a.k,
                      a.sos, d.tok[0], d.src[0], d.score[0], nullptr);
+  // the folded step with one attention block per utterance (k = 4 or 8 rows per block): the select
+  // of step l - 1 runs in step l's attention prologue (CASR_OPT_FUSE_SELECT; the last step's select
+  // is a launch of its own)
+  const bool fsel = a.fold && a.fuse_select && (a.k == 4 || a.k == 8) && attention_kpb(a.B, a.k, a.attn_kpb) == a.k;
   for (int l = 0; l < a.max_len; ++l) {
     // the folded step (CASR_OPT_DEC_FOLD): step 0's LSTMCell + attention, then per step the
     // attention with the cell prologue (l >= 1) and the fused GEMM
     hipError_t e;
-    if (!a.fold) e = decode_step(a, d, l, a.B, nullptr, s);
-    else if (l == 0) e = decode_step(a, d, 0, a.B, nullptr, s, nullptr, false);
-    else e = fold_attention_step(a, d, l, a.B, nullptr, false, GreedySel{}, s);
+    if (!a.fold) {
+      e = decode_step(a, d, l, a.B, nullptr, s);
+    } else if (l == 0) {
+      e = decode_step(a, d, 0, a.B, nullptr, s, nullptr, false);
+    } else {
+      const BeamSelArgs bs = beam_sel_args(a, d, l - 1);
+      e = fold_attention_step(a, d, l, a.B, nullptr, false, GreedySel{}, s, fsel ? &bs : nullptr);
+    }
     if (e != hipSuccess) return e;
     if (a.fold) fold_gemm_step(a, d, l, a.B, s);
+    if (fsel && l + 1 < a.max_len) continue;
     ProfScope ps(a.prof, CASR_K_SELECT, s);
     if (a.k <= 2) launch_beam_select<4>(a, d, l, s);
     else if (a.k <= 4) launch_beam_select<8>(a, d, l, s);

@@ -267,6 +267,55 @@ def test_fused_select_equals_select_launches(eng, eos_bias, graphs):
         assert bool(outs[1]["finished"].any()), "with the EOS bias some rows must finish early"
 
 
+@pytest.mark.parametrize("k,eos_bias,graphs", [(8, 0.0, False), (8, 12.0, True), (4, 12.0, False)])
+def test_beam_select_in_attention_equals_select_launches(eng, k, eos_bias, graphs):
+    """The folded beam step with one attention block per utterance (k = 4 or 8 at B = 256, R >= 1024
+    rows): the select of step l - 1 run in step l's attention prologue (default, attention.hip CELL 3)
+    and every select a launch of its own (CASR_OPT_FUSE_SELECT = 0) give the same tokens, lengths,
+    scores, step counts and finished-hypothesis records bit for bit, without and with early stops
+    (eos_bias).  Without graphs: the folded step is in effect (one LSTMCell launch, step 0's) and the
+    fused decode launches one select (the last step's) instead of one per step."""
+    if eng.requested != "s16x3":
+        pytest.skip("the beam fold, and with it the fused select, runs on the s16x3 images")
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True, eos_bias=eos_bias)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    B = 256
+    rs = np.random.RandomState(9)
+    frames = rs.randint(30, 300, size=B)
+    x = np.zeros((B, 300, 80), np.float32)
+    for b in range(B):
+        x[b, :frames[b]] = fbank_for(b, int(frames[b]))
+    feat, flen = eng.features(torch.from_numpy(x).to(eng.device),
+                              torch.from_numpy(frames.astype(np.int32)).to(eng.device))
+    eng.encode(feat, flen)
+    outs = []
+    try:
+        eng.set_graphs(graphs)
+        for fuse in (0, 1, 0):
+            eng.set_option("FUSE_SELECT", fuse)
+            if not graphs:
+                eng.profile(["select", "dec_lstm"])
+            bm = eng.beam(k)
+            rt, rsc, rv = eng.beam_records()
+            assert eng.device_flags() == 0
+            o = {n: v.cpu() for n, v in bm.items()}
+            o.update(rec_tokens=rt.cpu(), rec_score=rsc.cpu(), rec_valid=rv.cpu())
+            outs.append(o)
+            if not graphs:
+                prof = eng.profile_read()
+                assert prof["dec_lstm"][0] == 1, "the folded beam step"
+                assert prof["select"][0] == (1 if fuse else CFG.max_len)
+                eng.profile([])
+    finally:
+        eng.set_option("FUSE_SELECT", 1)
+        eng.set_graphs(2)
+    for o in outs[1:]:
+        for n in outs[0]:
+            assert torch.equal(outs[0][n], o[n]), n
+    if eos_bias:
+        assert int(outs[1]["steps"][0]) < CFG.max_len, "with the EOS bias the search must stop early"
+
+
 @pytest.mark.parametrize("B,layout", [(37, 0), (37, 1), (37, 2), (256, 0)])
 def test_persistent_recurrence_equals_per_step(eng, B, layout):
     """The persistent per-layer recurrence (granule hand-offs, either store flavour, ordinary or
