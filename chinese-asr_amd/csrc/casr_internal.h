@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 1, 0, 0, 1, 0, 0, 1};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 1, 0, 0, 1, 0, 0, 1, 1};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -262,7 +262,7 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
                             int residual, int s16, int32_t* err, uint32_t* trace, int layout, const Tuning& t,
                             hipStream_t s);
 hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc16, const float* b_attn,
-                           float* keysT, hipStream_t s);
+                           float* keysT, hipStream_t s, int rows = 1);
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s);
 

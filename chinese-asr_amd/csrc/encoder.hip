@@ -400,12 +400,145 @@ hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, cons
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ keys, row-streaming form
+// keys16_kernel (round 5, default; CASR_OPT_KEYS_ROWS = 0 keeps gemm_nt_kernel<KeysEpi, true>).  The
+// keys GEMM is N = A = 128 columns by K = C = 512 over B Tp rows: gemm_nt_kernel's 128 x 128 tiles
+// give 532 blocks at B = 256 for 512 slots (two per CU), so 20 blocks ran a second round and the
+// launch took two block times (94 us).  Here one workgroup per CU keeps W_enc's s16 image in
+// registers (wave w: columns 16 w .. 16 w + 15 over all 16 k-tiles, 128 VGPRs) and streams items of
+// 16 A rows (16 consecutive t of one utterance, 32 KB) through an LDS ring of four (three in
+// flight): [k-tile][16 rows][128 B], chunk c of a row's k-tile at slot c ^ ((row >> 1) & 7), filled
+// by LDS-DMA.  Each wave multiplies every item by its columns with the s16x3 MFMAs of
+// gemm_nt_kernel<KeysEpi, true> in the same k order, and the lane's four rows of one column are
+// four consecutive t: one float4 of keysT and one of e^{2 keys} (KeysEpi's arithmetic) per lane and
+// item, written by buffer stores whose lanes past the utterance's Tq slots are dropped by the
+// hardware, so every wave issues exactly two stores per item and the counted vmcnt waits stay exact.
+// Rows past Tp (the last item of an utterance) read row Tp - 1 and land in the pad slots
+// t in [Tp, Tq), which the attention never reads (masked past len), or are dropped.
+template <int VM>
+CASR_DEV void g16_vm_wait_k() {
+  static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
+}
+constexpr int KR_G = 16;                   // A rows per item
+constexpr int KR_KT = C / 32;              // 32-deep k-tiles
+constexpr int KR_IF = KR_KT * KR_G * 32;   // floats per item (32 KB)
+constexpr int KR_NBUF = 4;                 // ring slots (three items in flight)
+
+__global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict__ enc16, const float* __restrict__ w16,
+                                                        const float* __restrict__ bias, float* __restrict__ keysT,
+                                                        int B, int Tp, int Tq) {
+  __shared__ __attribute__((aligned(16))) float ring[KR_NBUF * KR_IF];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
+  const int ng = (Tp + KR_G - 1) / KR_G, NI = B * ng, G = gridDim.x;
+  const int nitems = blockIdx.x < NI ? (NI - 1 - blockIdx.x) / G + 1 : 0;
+  // W fragments of columns 16 w + r: lane (r, g) holds hi / lo chunk g of every k-tile
+  f16x8 wh[KR_KT], wl[KR_KT];
+  {
+    const float* wr = w16 + (size_t)(16 * w + r) * C + 4 * g;
+#pragma unroll
+    for (int kt = 0; kt < KR_KT; ++kt) {
+      wh[kt] = *reinterpret_cast<const f16x8*>(wr + kt * 32);
+      wl[kt] = *reinterpret_cast<const f16x8*>(wr + kt * 32 + 16);
+    }
+  }
+  const float bv = bias[16 * w + r];
+  // item q of this block: utterance b, rows t = 16 j .. 16 j + 15
+  auto item = [&](int q, int& b, int& j) {
+    const int x = blockIdx.x + q * G;
+    b = x / ng;
+    j = x - b * ng;
+  };
+  // 32 DMA instructions of 1 KB per item (k-tile kt, rows 8 h .. 8 h + 7), four per wave
+  auto stage = [&](int q) {
+    int b, j;
+    item(q, b, j);
+    float* dst = ring + (q % KR_NBUF) * KR_IF;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = w + 8 * u, kt = i >> 1, h = i & 1;
+      const int row = 8 * h + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+      const int t = min(KR_G * j + row, Tp - 1);
+      lds_dma16(enc16 + ((size_t)b * Tp + t) * C + kt * 32 + 4 * c, dst + (kt * KR_G + 8 * h) * 32);
+    }
+  };
+  // VMEM operations this wave issued after the DMA of item q, at the top of iteration q: each
+  // iteration i issues the DMA of item i + 3 (when it exists, 4 operations) and then the item's two
+  // stores; the prologue issues the DMAs of items 0 .. 2
+  auto younger = [&](int q) {
+    auto dma = [&](int i) { return i + KR_NBUF - 1 < nitems ? 4 : 0; };
+    int n = 0;
+    if (q < KR_NBUF - 1) {
+      n += 4 * (min(KR_NBUF - 1, nitems) - 1 - q);
+      for (int i = 0; i < q; ++i) n += dma(i) + 2;
+    } else {
+      n += 2;
+      for (int i = q - KR_NBUF + 2; i < q; ++i) n += dma(i) + 2;
+    }
+    return n;
+  };
+  const size_t eoff = (size_t)B * A * Tq;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(keysT, 0, (int)(2 * eoff * 4), 0x00020000);
+  for (int q = 0; q < KR_NBUF - 1 && q < nitems; ++q) stage(q);
+  for (int q = 0; q < nitems; ++q) {
+    const int y = younger(q);
+    if (y >= 14) g16_vm_wait_k<14>();
+    else if (y >= 12) g16_vm_wait_k<12>();
+    else if (y >= 10) g16_vm_wait_k<10>();
+    else if (y >= 8) g16_vm_wait_k<8>();
+    else if (y >= 6) g16_vm_wait_k<6>();
+    else if (y >= 4) g16_vm_wait_k<4>();
+    else if (y >= 2) g16_vm_wait_k<2>();
+    else g16_vm_wait_k<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's part of item q landed; item q - 1's slot is free
+    asm volatile("" ::: "memory");
+    if (q + KR_NBUF - 1 < nitems) stage(q + KR_NBUF - 1);
+    const float* as = ring + (q % KR_NBUF) * KR_IF;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accx = {0.f, 0.f, 0.f, 0.f};
+    const int sw = (r >> 1) & 7;
+#pragma unroll
+    for (int kt = 0; kt < KR_KT; ++kt) {
+      const float* ar = as + (kt * KR_G + r) * 32;
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(ar + ((g ^ sw) << 2));
+      const f16x8 al = *reinterpret_cast<const f16x8*>(ar + (((4 + g) ^ sw) << 2));
+      mfma_s16(ah, al, wh[kt], wl[kt], acc, accx);
+    }
+    int b, j;
+    item(q, b, j);
+    const int t0 = KR_G * j + 4 * g;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = s16_combine(acc[e], accx[e]) + bv;
+    // lanes whose quad lies past the utterance's Tq slots store out of range (dropped)
+    const uint32_t off = t0 < Tq ? (uint32_t)((((size_t)b * A + 16 * w + r) * Tq + t0) * 4) : 0xFFFFFFF0u;
+    const float4 kq = make_float4(v[0], v[1], v[2], v[3]);
+    const float4 eq = make_float4(split_exp2x(v[0]), split_exp2x(v[1]), split_exp2x(v[2]), split_exp2x(v[3]));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, kq), rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, eq), rs,
+                                           t0 < Tq ? off + (uint32_t)(eoff * 4) : 0xFFFFFFF0u, 0, 0);
+  }
+}
+
 // keys from the s16 row image of the encoder output (written by the last persistent layer) and
-// of wencT: s16x3 products, same KeysEpi store
+// of wencT: s16x3 products, same KeysEpi store (rows = 1: keys16_kernel, the default)
 hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc16, const float* b_attn,
-                           float* keysT, hipStream_t s) {
+                           float* keysT, hipStream_t s, int rows) {
   const int M = B * Tp;
   if (M <= 0 || C % GB_K != 0) return hipErrorInvalidValue;
+  if (rows) {
+    static int ncu = [] {
+      int dev = 0, v = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+      return v > 0 ? v : 256;
+    }();
+    const int Tq = (Tp + 3) & ~3, NI = B * ((Tp + KR_G - 1) / KR_G);
+    if ((size_t)2 * B * A * Tq * 4 >= 0xFFFFFFF0u) return hipErrorInvalidValue;  // 32-bit buffer offsets
+    hipLaunchKernelGGL(keys16_kernel, dim3(std::min(NI, ncu)), dim3(512), 0, s, enc16, wenc16, b_attn, keysT, B, Tp,
+                       Tq);
+    return hipGetLastError();
+  }
   KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3, B};
   const TileOrder order = tile_order(A / GB_N, (M + GB_M - 1) / GB_M, C);
   hipLaunchKernelGGL((gemm_nt_kernel<KeysEpi, true>), dim3(order.blocks()), dim3(256), 0, s, enc16, C, wenc16,

@@ -237,6 +237,10 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            stage exchanges (round 4).  The same butterflies in the same order
  *   CASR_OPT_ATTN_KPB        beam rows per attention block at k > 2: 0 auto (8 at B >= 256 and
  *                            k >= 8, else 4), 4 or 8
+ *   CASR_OPT_KEYS_ROWS       1: the s16x3 keys GEMM keeps W_enc in registers and streams 16-row
+ *                            items of the encoder output through LDS, one workgroup per CU (default,
+ *                            round 5); 0: 128 x 128 tiles (gemm_nt_kernel).  The same MFMAs in the
+ *                            same order
  * Two options select numerics variants instead (the same token ids, floating-point results within
  * the stated tolerances, not bit for bit; tests/test_gpu_parity.py compares each pair):
  *   CASR_OPT_ATTN_DIRECT     0: attention scores in the split exponential form 1 - 2 / (1 + e^{2k}
@@ -288,7 +292,8 @@ enum {
   CASR_OPT_REC_COOP_REFUSE = 11,
   CASR_OPT_DIAG_COLD = 12,
   CASR_OPT_LOGMEL_Q16 = 13,
-  CASR_OPT_COUNT = 14
+  CASR_OPT_KEYS_ROWS = 14,
+  CASR_OPT_COUNT = 15
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

@@ -594,6 +594,39 @@ def test_attention_split_form_vs_direct(eng, name):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B,T", [(37, 400), (256, 800)])
+def test_keys_row_streaming_equals_tiles(eng, B, T):
+    """The s16x3 keys GEMM in its two forms (CASR_OPT_KEYS_ROWS: W_enc in registers and 16-row items
+    streamed through LDS, the default; or 128 x 128 tiles) gives the same keys and e^{2 keys} bit for
+    bit (same MFMAs, same k order): the keys over every Tp slot, and greedy tokens, scores and
+    alignments (which read e^{2 keys} through the split score form).  Ragged lengths at B = 37
+    (Tp = 133: a partial last item per utterance), and the metric's B = 256, T = 800."""
+    if eng.requested != "s16x3":
+        pytest.skip("the f32 arithmetic keeps the f32 keys GEMM")
+    bind(eng, "peaked")
+    rs = np.random.RandomState(11)
+    frames = rs.randint(max(30, T // 2), T + 1, size=B) if B < 256 else np.full(B, T)
+    x = np.zeros((B, T, 80), np.float32)
+    for b in range(B):
+        x[b, :frames[b]] = fbank_for(b, int(frames[b]))
+    feat, flen = eng.features(torch.from_numpy(x).to(eng.device),
+                              torch.from_numpy(frames.astype(np.int32)).to(eng.device))
+    outs = []
+    try:
+        for rows in (1, 0, 1):
+            eng.set_option("KEYS_ROWS", rows)
+            eng.encode(feat, flen)
+            keys = eng.encoder_results()[3].cpu()
+            g = eng.greedy(alignment=True)
+            assert eng.device_flags() == 0
+            outs.append([keys] + [g[n].cpu() for n in ("tokens", "accum", "alignment")])
+    finally:
+        eng.set_option("KEYS_ROWS", 1)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("name", ["plain", "peaked"])
 def test_decode_fold_vs_three_launches(eng, name):
     """The folded greedy step (CASR_OPT_DEC_FOLD, default under s16x3: the projection GEMM also
