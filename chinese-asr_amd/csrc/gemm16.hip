@@ -422,10 +422,14 @@ CASR_DEV unsigned long long pp_stamp() {
   __builtin_amdgcn_sched_barrier(0);
   return t;
 }
-template <int DIAG = 0, int PRIO = 1, int SG = 0, int AGPR = 0>
+// KM (tools/probes only so far): A and W images 16-k-block major, [Kp / 16][rows][16 hi | 16 lo]
+// halves, so a stage of 16 rows is 1 KB contiguous (whole 128-B lines) instead of 16 half lines;
+// Mimg = the A image's row count
+template <int DIAG = 0, int PRIO = 1, int SG = 0, int AGPR = 0, bool KM = false>
 __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
                                                            const float* __restrict__ bias, float* __restrict__ Cout,
-                                                           int M, int N, int Kp, Order16 order, int total, int nk) {
+                                                           int M, int N, int Kp, Order16 order, int total, int nk,
+                                                           int Mimg = 0) {
   __shared__ __attribute__((aligned(16))) float lds[PP_LDS];
   // AGPR: an AGPR clobber keeps the accumulation registers available, so hipcc picks the MFMA form
   // with the accumulators in AGPRs (C / D traffic off the VGPR file the partner's LDS returns use)
@@ -454,20 +458,20 @@ __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restri
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = wave * 32 + i * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
-    coff[i] = (c >> 1) * 16 + (c & 1) * 4;
-    vw[i] = (uint32_t)(row * Kp + coff[i]) * 4u;  // N % 256 == 0 (host check): no clamp
+    coff[i] = KM ? 4 * c : (c >> 1) * 16 + (c & 1) * 4;
+    vw[i] = (uint32_t)(row * (KM ? 16 : Kp) + coff[i]) * 4u;  // N % 256 == 0 (host check): no clamp
   }
   auto a_offsets = [&](int m, uint32_t (&va)[2]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = wave * 32 + i * 16 + (lane >> 2);
-      va[i] = (uint32_t)(min(row, M - 1 - m * G16_M) * Kp + coff[i]) * 4u;
+      va[i] = (uint32_t)(min(row, M - 1 - m * G16_M) * (KM ? 16 : Kp) + coff[i]) * 4u;
     }
   };
   auto stage_dma = [&](int b, int n, int m, int s, int tpar, const uint32_t (&va)[2]) {
     const int kb = (s >> 1) * 32 + (s & 1) * 8;  // float offset of this stage's hi piece in the row image
-    const float* sa = A16 + (size_t)m * G16_M * Kp + kb;
-    const float* sw = W16 + (size_t)n * G16_N * Kp + kb;
+    const float* sa = KM ? A16 + ((size_t)s * Mimg + (size_t)m * G16_M) * 16 : A16 + (size_t)m * G16_M * Kp + kb;
+    const float* sw = KM ? W16 + ((size_t)s * N + (size_t)n * G16_N) * 16 : W16 + (size_t)n * G16_N * Kp + kb;
     const uint32_t l0 = lds_u32 + (uint32_t)(b * PP_STAGE + wave * 32 * PP_ROWF) * 4u;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -626,6 +630,123 @@ __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restri
 }
 
 
+// ---- balanced tail (round 5, CASR_OPT_GEMM16_TAIL = 2, default): the rows after the persistent
+// kernel's whole rounds as (32 RT)-row x 128-column tiles, RT picked so that they fill the CUs in one
+// round (B = 256: 2,560 rows = 16 row blocks of 160 rows x 16 column blocks = 256 tiles; TAIL = 1 ran
+// them as 160 half tiles of 128 x 256 on a two-buffer ring drained by __syncthreads, 36 us).  Four
+// waves, wave w: columns 32 w .. 32 w + 31 of the tile over its RT row tiles of 32; a ring of four
+// 32-deep stages [A 32 RT rows | W 128 rows] x 128 B (three in flight), LDS-DMA from inline asm with
+// counted vmcnt waits and a raw s_barrier per stage.  The MFMAs per accumulator are compute() of
+// gemm16_bias_kernel (same fragments, order and 2^11 scaling), and the epilogue its slab form: the
+// same bits.
+template <int RT>
+__global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
+                                                             const float* __restrict__ bias, float* __restrict__ Cout,
+                                                             int M, int N, int Kp) {
+  constexpr int BM = 32 * RT, BN = 128, ROWS = BM + BN, STF = ROWS * G16_K;  // floats per stage
+  constexpr int NBUF = 4, NI = ROWS / 8, PW = (NI + 3) / 4;  // DMA instructions per stage / per wave
+  static_assert(NBUF * STF * 4 <= 160 * 1024 && (NBUF - 2) * PW < 64, "ring fits the LDS; vmcnt range");
+  __shared__ __attribute__((aligned(16))) float ring[NBUF * STF];
+  const int ncb = N / BN, mt = blockIdx.x / ncb, nt = blockIdx.x - mt * ncb;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, hsel = lane >> 5;
+  const int cnt = (NI - wave + 3) / 4;  // DMA instructions this wave issues per stage (i = wave + 4 j < NI)
+  f32x16 acc[RT];
+#pragma unroll
+  for (int i = 0; i < RT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+  auto stage = [&](int kt) {
+    float* dst = ring + (kt % NBUF) * STF;
+    const int k0 = kt * G16_K;
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const int i = wave + 4 * j;
+      if (i < NI) {
+        const int row = 8 * i + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+        const float* src = row < BM ? A16 + (size_t)min(m0 + row, M - 1) * Kp + k0 + 4 * c
+                                    : W16 + (size_t)(n0 + row - BM) * Kp + k0 + 4 * c;
+        lds_dma16(src, dst + 8 * i * G16_K);
+      }
+    }
+  };
+  const _Float16 two11 = (_Float16)2048.0f;
+  auto compute = [&](const float* src) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 2 * ks + hsel;  // 16-B chunk of this lane's 8 k (hi); lo is chunk 4 + ch
+      const int wrow = BM + wave * 32 + r32, wsw = (wrow >> 1) & 7;
+      const f16x8 wh = *reinterpret_cast<const f16x8*>(src + wrow * G16_K + ((ch ^ wsw) << 2));
+      const f16x8 wl = *reinterpret_cast<const f16x8*>(src + wrow * G16_K + (((4 + ch) ^ wsw) << 2));
+      const f16x8 w1 = wh * two11;
+#pragma unroll
+      for (int tm = 0; tm < RT; ++tm) {
+        const int row = tm * 32 + r32, sw = (row >> 1) & 7;
+        const f16x8 ah = *reinterpret_cast<const f16x8*>(src + row * G16_K + ((ch ^ sw) << 2));
+        const f16x8 al = *reinterpret_cast<const f16x8*>(src + row * G16_K + (((4 + ch) ^ sw) << 2));
+        acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w1, acc[tm], 0, 0, 0);
+        acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl, acc[tm], 0, 0, 0);
+        acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh, acc[tm], 0, 0, 0);
+      }
+    }
+  };
+  const int nk = Kp / G16_K;
+  for (int kt = 0; kt < NBUF - 1 && kt < nk; ++kt) stage(kt);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int younger = min(NBUF - 2, nk - 1 - kt) * cnt;  // this wave's DMA issued after stage kt's
+    if (younger >= 2 * PW) g16_vm_wait<2 * PW>();
+    else if (younger >= 2 * PW - 2) g16_vm_wait<2 * PW - 2>();
+    else if (younger >= PW) g16_vm_wait<PW>();
+    else if (younger >= PW - 1) g16_vm_wait<PW - 1>();
+    else g16_vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage kt landed for every wave; stage kt - 1's buffer is no longer read
+    asm volatile("" ::: "memory");
+    if (kt + NBUF - 1 < nk) stage(kt + NBUF - 1);
+    compute(ring + (kt % NBUF) * STF);
+  }
+  // epilogue: RT 32-row slabs through the ring, stored as 512-B row segments (+ bias)
+  constexpr int LDC = BN + 4;
+  const int c4 = tid & 31, r0 = tid >> 5;  // 32 float4 per row, 8 rows per pass
+  const float4 b4 = *reinterpret_cast<const float4*>(bias + n0 + c4 * 4);
+#pragma unroll
+  for (int tm = 0; tm < RT; ++tm) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      ring[((e & 3) + 8 * (e >> 2) + 4 * hsel) * LDC + wave * 32 + r32] = acc[tm][e] * S16_LO_INV;
+    __syncthreads();
+#pragma unroll
+    for (int row = r0; row < 32; row += 8) {
+      const int gr = m0 + tm * 32 + row;
+      if (gr < M) {
+        const float4 v = *reinterpret_cast<const float4*>(ring + row * LDC + c4 * 4);
+        *reinterpret_cast<float4*>(Cout + (size_t)gr * N + n0 + c4 * 4) =
+            make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
+      }
+    }
+  }
+}
+
+// tail rows [r0, M) of the input projection as gemm16_tail_kernel tiles: false when they do not fit
+// one round of ncu workgroups (the caller then takes the half-tile launch)
+static bool launch_tail_balanced(const float* A16, const float* W16, const float* bias, float* Gin, int Mt, int N, int Kp,
+                                 int ncu, hipStream_t s) {
+  if (Mt <= 0 || N % 128 != 0) return false;
+  const int units = (Mt + 31) / 32 * (N / 128);
+  const int RT = (units + ncu - 1) / ncu;
+  if (RT > 5) return false;
+  const int blocks = (Mt + 32 * RT - 1) / (32 * RT) * (N / 128);
+  switch (RT) {
+    case 1: hipLaunchKernelGGL(gemm16_tail_kernel<1>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
+    case 2: hipLaunchKernelGGL(gemm16_tail_kernel<2>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
+    case 3: hipLaunchKernelGGL(gemm16_tail_kernel<3>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
+    case 4: hipLaunchKernelGGL(gemm16_tail_kernel<4>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
+    default: hipLaunchKernelGGL(gemm16_tail_kernel<5>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
+  }
+  return true;
+}
+
 }  // namespace
 
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
@@ -666,7 +787,7 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     if (persist == 2) {  // ping-pong form: 16-deep stages
       const int nk16 = (K > 0 && K <= Kp ? K + 15 : Kp) / 16;
       hipLaunchKernelGGL((gemm16_pp_kernel<0, 1>), dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
-                         N, Kp, om, total, nk16);
+                         N, Kp, om, total, nk16, M);
     } else {
       hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
                          N, Kp, om, total, nk);
@@ -674,6 +795,8 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     if (NMm < NM) {
       const size_t r0 = (size_t)NMm * G16_M;
       const int Mt = M - (int)r0, NMt = (Mt + 127) / 128;
+      if (tail == 2 && launch_tail_balanced(X16 + r0 * Kp, W16, bias, Gin + r0 * N, Mt, N, Kp, ncu, s))
+        return hipGetLastError();
       const Order16 ot{NB, NMt, NG};  // XCD grouping of the tail: the same column slices per XCD
       hipLaunchKernelGGL((gemm16_bias_kernel<4, 1>), dim3(ot.blocks()), dim3(256), 0, s, X16 + r0 * Kp, W16, bias,
                          Gin + r0 * N, Mt, N, Kp, ot);

@@ -213,8 +213,10 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  * every value of every option gives the same results bit for bit (tests/test_gpu_parity.py sweeps
  * them), so an option only ever changes speed.  Options are read at each call and are part of the
  * keys of the captured hipGraphs, so changing one between calls takes effect at the next call.
- *   CASR_OPT_FUSE_SELECT     1: greedy select of step l fused into step l+1's LSTMCell (default);
- *                            0: every select a launch of its own
+ *   CASR_OPT_FUSE_SELECT     1 (default): the select of step l runs inside a kernel of step l + 1:
+ *                            greedy, the LSTMCell (three-launch step) or the attention (folded
+ *                            step); beam 4 or 8 with one attention block per utterance (folded
+ *                            step), the attention.  0: every select a launch of its own
  *   CASR_OPT_REC_LAYOUT      persistent recurrence workgroup shape: 0 auto (default: 16 rows x 16
  *                            units when that grid fits one workgroup per CU, else 32 x 16), 1 32x16,
  *                            2 16x32, 3 16x16
@@ -230,8 +232,9 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *   CASR_OPT_GEMM16_PERSIST  s16x3 input-projection kernel: 2 persistent ping-pong form (default: two
  *                            wave groups one barrier apart, 16-deep stages on a ring of four); 1
  *                            persistent, 32-deep stages on two buffers; 0 one workgroup per tile
- *   CASR_OPT_GEMM16_TAIL     1: the persistent kernel takes whole rounds of tiles, the rows after
- *                            them go to one launch of half tiles (default); 0: partial last round
+ *   CASR_OPT_GEMM16_TAIL     2 (default): the persistent kernel takes whole rounds of tiles and the
+ *                            rows after them go to one round of (32 RT) x 128 tiles; 1: to one
+ *                            launch of 128 x 256 half tiles; 0: partial last round
  *   CASR_OPT_LOGMEL_Q16      1: casr_log_mel runs 16 lanes per frame, 16 FFT points per lane, one
  *                            stage exchange per frame (default, round 5); 0: one wave per frame, three
  *                            stage exchanges (round 4).  The same butterflies in the same order

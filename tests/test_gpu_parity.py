@@ -771,7 +771,9 @@ def test_input_gemm_tail_split_bitwise(eng, B):
     (B = 256 and 128: 80 / 40 tiles past the last whole round; B = 37: 48 tiles in one partial round).
     Round 5: the ping-pong persistent kernel (CASR_OPT_GEMM16_PERSIST = 2, the default: 16-deep
     stages, two staggered wave groups, buffer stores that drop rows past M) with and without the
-    tail split, against the round-2 persistent kernel and the per-tile kernel."""
+    tail split, against the round-2 persistent kernel and the per-tile kernel; and the balanced tail
+    (CASR_OPT_GEMM16_TAIL = 2, the default: one round of 160 x 128 tiles at B = 256, 96 x 128 at
+    B = 128) against the half tiles."""
     if eng.precision() != "s16x3":
         pytest.skip("the split-f16 input GEMM only")
     bind(eng, "peaked")
@@ -780,14 +782,14 @@ def test_input_gemm_tail_split_bitwise(eng, B):
     fb, fr = batch_fbank(frames, eng.device)
     outs = []
     try:
-        for tail, persist in ((1, 2), (0, 2), (1, 1), (0, 1), (1, 0)):
+        for tail, persist in ((2, 2), (1, 2), (0, 2), (2, 1), (1, 1), (0, 1), (1, 0)):
             eng.set_option("GEMM16_TAIL", tail)
             eng.set_option("GEMM16_PERSIST", persist)
             eng.encode_fbank(fb, fr)
             assert eng.device_flags() == 0
             outs.append([t.cpu() for t in eng.encoder_results()])
     finally:
-        eng.set_option("GEMM16_TAIL", 1)
+        eng.set_option("GEMM16_TAIL", 2)
         eng.set_option("GEMM16_PERSIST", 2)
     for got in outs[1:]:
         for a, b in zip(outs[0], got):

@@ -46,10 +46,28 @@ static void make_image(std::vector<uint16_t>& img, int rows, int Kp, int K, unsi
     }
 }
 
+// the same image 16-k-block major: [Kp / 16][rows][16 hi | 16 lo] halves
+static void to_km(const std::vector<uint16_t>& img, std::vector<uint16_t>& km, int rows, int Kp) {
+  km.assign(img.size(), 0);
+  for (int r = 0; r < rows; ++r)
+    for (int k = 0; k < Kp; ++k) {
+      const uint16_t* t = img.data() + ((size_t)r * Kp + (k / 32) * 32) * 2;
+      uint16_t* o = km.data() + ((size_t)(k / 16) * rows + r) * 32;
+      o[k % 16] = t[k % 32];
+      o[16 + k % 16] = t[32 + k % 32];
+    }
+}
+
 static int ncu() {
   int v = 0;
   CK(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, 0));
   return v;
+}
+
+template <int D>
+static void run_pp(int grid, const float* A, const float* W, const float* B, float* C, int M, int N, int Kp, Order16 o,
+                   int nk) {
+  hipLaunchKernelGGL((gemm16_pp_kernel<D>), dim3(grid), dim3(512), 0, 0, A, W, B, C, M, N, Kp, o, o.blocks(), nk, M);
 }
 
 template <class Kern>
@@ -90,9 +108,18 @@ int main(int argc, char** argv) {
       make_image(w, N, Kp, K, 2u, 0.05f);
       std::vector<float> bias(N);
       for (int i = 0; i < N; ++i) bias[i] = 0.001f * (i % 97) - 0.05f;
-      float *dA, *dW, *dB, *dC0, *dC1;
+      float *dA, *dW, *dB, *dC0, *dC1, *dAk, *dWk;
       CK(hipMalloc(&dA, a.size() * 2));
       CK(hipMalloc(&dW, w.size() * 2));
+      {
+        std::vector<uint16_t> ak, wk;
+        to_km(a, ak, M, Kp);
+        to_km(w, wk, N, Kp);
+        CK(hipMalloc(&dAk, ak.size() * 2));
+        CK(hipMalloc(&dWk, wk.size() * 2));
+        CK(hipMemcpy(dAk, ak.data(), ak.size() * 2, hipMemcpyHostToDevice));
+        CK(hipMemcpy(dWk, wk.data(), wk.size() * 2, hipMemcpyHostToDevice));
+      }
       CK(hipMalloc(&dB, N * 4));
       CK(hipMalloc(&dC0, (size_t)M * N * 4 + 4096));
       CK(hipMalloc(&dC1, (size_t)M * N * 4 + 4096));
@@ -105,6 +132,10 @@ int main(int argc, char** argv) {
       const Order16 o{NB, NM, NG};
       const int nk32 = (K + 31) / 32, nk16 = (K + 15) / 16;
       const int grid = std::min(o.blocks(), G);
+      auto run_km = [&](float* C) {
+        hipLaunchKernelGGL((gemm16_pp_kernel<0, 1, 0, 0, true>), dim3(grid), dim3(512), 0, 0, dAk, dWk, dB, C, M, N, Kp, o,
+                           o.blocks(), nk16, M);
+      };
       // reference: the persistent kernel
       CK(hipMemset(dC0, 0, (size_t)M * N * 4 + 4096));
       run(gemm16_persist_kernel<0>, grid, dA, dW, dB, dC0, M, N, Kp, o, nk32);
@@ -115,7 +146,8 @@ int main(int argc, char** argv) {
       size_t bad = 0;
       for (int r = 0; r < reps; ++r) {
         CK(hipMemset(dC1, 0xFF, (size_t)M * N * 4 + 4096));
-        if (r & 1) run(gemm16_pp_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+        if (r % 3 == 1) run_pp<0>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+        else if (r % 3 == 2) run_km(dC1);
         else run(gemm16_w4_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(c1.data(), dC1, c1.size() * 4, hipMemcpyDeviceToHost));
@@ -129,29 +161,31 @@ int main(int argc, char** argv) {
           if (__builtin_bit_cast(uint32_t, c1[i]) != 0xFFFFFFFFu) ++diff;
         bad += diff;
       }
-      printf("Kp %d M %d: w4 (even reps) / pp (odd) vs persist: %zu differing outputs over %d reps\n", Kp, M, bad, reps);
+      printf("Kp %d M %d: w4 / pp / pp-km (reps mod 3) vs persist: %zu differing outputs over %d reps\n", Kp, M, bad, reps);
       if (M == 256 * 266) {
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         const char* names[] = {"persist", "pp", "pp:no-dma", "pp:no-mfma", "pp:no-stores", "pp:contig",
                                "pp:contig-no-mfma", "pp:dma-only", "pp:mfma+lds", "pp:lds-only", "w4",
-                               "w4:no-dma", "w4:no-mfma", "w4:no-stores", "w4:mfma+lds"};
+                               "w4:no-dma", "w4:no-mfma", "w4:no-stores", "w4:mfma+lds", "pp:km"};
+        const int nv = getenv("PP_ONLY") ? 0 : 15;
         for (int rep = 0; rep < 3; ++rep)
-          for (int v = 0; v < 15; ++v) {
+          for (int v = nv ? 0 : 1; v < 16; v = (nv || v != 1) ? v + 1 : 15) {
             const int iters = 10;
             CK(hipEventRecord(e0));
             for (int i = 0; i < iters; ++i) {
               if (v == 0) run(gemm16_persist_kernel<0>, grid, dA, dW, dB, dC0, M, N, Kp, o, nk32);
-              else if (v == 1) run(gemm16_pp_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 2) run(gemm16_pp_kernel<1>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 3) run(gemm16_pp_kernel<2>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 4) run(gemm16_pp_kernel<4>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 5) run(gemm16_pp_kernel<8>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 6) run(gemm16_pp_kernel<10>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 7) run(gemm16_pp_kernel<6>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 8) run(gemm16_pp_kernel<5>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
-              else if (v == 9) run(gemm16_pp_kernel<7>, grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 1) run_pp<0>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 2) run_pp<1>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 3) run_pp<2>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 4) run_pp<4>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 5) run_pp<8>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 6) run_pp<10>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 7) run_pp<6>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 8) run_pp<5>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 9) run_pp<7>(grid, dA, dW, dB, dC1, M, N, Kp, o, nk16);
+              else if (v == 15) run_km(dC1);
               else if (v == 10) run(gemm16_w4_kernel<0>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
               else if (v == 11) run(gemm16_w4_kernel<1>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
               else if (v == 12) run(gemm16_w4_kernel<2>, grid, dA, dW, dB, dC1, M, N, Kp, o, 2 * nk32, 256);
@@ -169,6 +203,8 @@ int main(int argc, char** argv) {
       }
       CK(hipFree(dA));
       CK(hipFree(dW));
+      CK(hipFree(dAk));
+      CK(hipFree(dWk));
       CK(hipFree(dB));
       CK(hipFree(dC0));
       CK(hipFree(dC1));
