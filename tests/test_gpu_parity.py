@@ -267,14 +267,17 @@ def test_fused_select_equals_select_launches(eng, eos_bias, graphs):
         assert bool(outs[1]["finished"].any()), "with the EOS bias some rows must finish early"
 
 
-@pytest.mark.parametrize("k,eos_bias,graphs", [(8, 0.0, False), (8, 12.0, True), (4, 12.0, False)])
+@pytest.mark.parametrize("k,eos_bias,graphs", [(8, 0.0, False), (8, 12.0, True), (8, 40.0, False), (4, 40.0, True)])
 def test_beam_select_in_attention_equals_select_launches(eng, k, eos_bias, graphs):
     """The folded beam step with one attention block per utterance (k = 4 or 8 at B = 256, R >= 1024
     rows): the select of step l - 1 run in step l's attention prologue (default, attention.hip CELL 3)
     and every select a launch of its own (CASR_OPT_FUSE_SELECT = 0) give the same tokens, lengths,
-    scores, step counts and finished-hypothesis records bit for bit, without and with early stops
-    (eos_bias).  Without graphs: the folded step is in effect (one LSTMCell launch, step 0's) and the
-    fused decode launches one select (the last step's) instead of one per step."""
+    scores, step counts and finished-hypothesis records bit for bit, without EOS bias, with finished
+    hypotheses (eos_bias 12: the search still runs all 40 steps at B = 256) and with an early stop
+    (eos_bias 40: every utterance's top candidate ends early, so the fused attention of the step after
+    the last select runs on counters it cannot know complete).  Without graphs: the folded step is in
+    effect (one LSTMCell launch, step 0's) and the fused decode launches one select (the last step's)
+    instead of one per step."""
     if eng.requested != "s16x3":
         pytest.skip("the beam fold, and with it the fused select, runs on the s16x3 images")
     enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True, eos_bias=eos_bias)
@@ -312,8 +315,10 @@ def test_beam_select_in_attention_equals_select_launches(eng, k, eos_bias, graph
     for o in outs[1:]:
         for n in outs[0]:
             assert torch.equal(outs[0][n], o[n]), n
-    if eos_bias:
+    if eos_bias >= 40:
         assert int(outs[1]["steps"][0]) < CFG.max_len, "with the EOS bias the search must stop early"
+    elif eos_bias:
+        assert bool(outs[1]["rec_valid"].any()), "with the EOS bias hypotheses finish"
 
 
 @pytest.mark.parametrize("B,layout", [(37, 0), (37, 1), (37, 2), (256, 0)])
