@@ -420,6 +420,11 @@ CASR_DEV void g16_vm_wait_k() {
   static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
   __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (15 << 8) | ((VM >> 4) << 14));
 }
+// (diagnostic builds only, tools/probes/keys_probe.hip: bit 0 drops the item DMA, bit 1 the MFMAs,
+// bit 2 the stores; the results are then wrong)
+#ifndef CASR_KR_DIAG
+#define CASR_KR_DIAG 0
+#endif
 constexpr int KR_G = 16;                   // A rows per item
 constexpr int KR_KT = C / 32;              // 32-deep k-tiles
 constexpr int KR_IF = KR_KT * KR_G * 32;   // floats per item (32 KB)
@@ -459,7 +464,7 @@ __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict_
       const int i = w + 8 * u, kt = i >> 1, h = i & 1;
       const int row = 8 * h + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
       const int t = min(KR_G * j + row, Tp - 1);
-      lds_dma16(enc16 + ((size_t)b * Tp + t) * C + kt * 32 + 4 * c, dst + (kt * KR_G + 8 * h) * 32);
+      if (!(CASR_KR_DIAG & 1)) lds_dma16(enc16 + ((size_t)b * Tp + t) * C + kt * 32 + 4 * c, dst + (kt * KR_G + 8 * h) * 32);
     }
   };
   // VMEM operations this wave issued after the DMA of item q, at the top of iteration q: each
@@ -502,7 +507,8 @@ __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict_
       const float* ar = as + (kt * KR_G + r) * 32;
       const f16x8 ah = *reinterpret_cast<const f16x8*>(ar + ((g ^ sw) << 2));
       const f16x8 al = *reinterpret_cast<const f16x8*>(ar + (((4 + g) ^ sw) << 2));
-      mfma_s16(ah, al, wh[kt], wl[kt], acc, accx);
+      if (!(CASR_KR_DIAG & 2)) mfma_s16(ah, al, wh[kt], wl[kt], acc, accx);
+      else acc[0] += (float)ah[0] + (float)al[1];
     }
     int b, j;
     item(q, b, j);
@@ -514,9 +520,10 @@ __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict_
     const uint32_t off = t0 < Tq ? (uint32_t)((((size_t)b * A + 16 * w + r) * Tq + t0) * 4) : 0xFFFFFFF0u;
     const float4 kq = make_float4(v[0], v[1], v[2], v[3]);
     const float4 eq = make_float4(split_exp2x(v[0]), split_exp2x(v[1]), split_exp2x(v[2]), split_exp2x(v[3]));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, kq), rs, off, 0, 0);
+    const uint32_t off2 = (CASR_KR_DIAG & 4) ? 0xFFFFFFF0u : off;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, kq), rs, off2, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, eq), rs,
-                                           t0 < Tq ? off + (uint32_t)(eoff * 4) : 0xFFFFFFF0u, 0, 0);
+                                           t0 < Tq && !(CASR_KR_DIAG & 4) ? off + (uint32_t)(eoff * 4) : 0xFFFFFFF0u, 0, 0);
   }
 }
 
