@@ -117,9 +117,23 @@ class _StubLM:
     """Deterministic stand-in for kenlm.LanguageModel.score (main.py:82, model.py:755): KenLM and
     an LM file are absent offline.  Tokens arrive as private-use characters (id -> U+E000 + id)."""
 
+    def __init__(self):
+        self._r = {}  # word -> its id % 97 (filled on first sight)
+
     def score(self, s, bos=True):
-        ids = [ord(w) - 0xE000 for w in s.split(" ") if w]
-        return -0.37 * len(ids) - 0.011 * sum(i % 97 for i in ids) - (0.5 if bos else 0.0)
+        # -0.37 n - 0.011 sum(id % 97) - 0.5 bos over the words' ids (the same integer sum and float
+        # operations as the per-call form, with each word's term looked up once it has been seen)
+        ws = s.split(" ")
+        if "" in ws:
+            ws = [w for w in ws if w]
+        r = self._r
+        try:
+            tot = sum(map(r.__getitem__, ws))
+        except KeyError:
+            for w in ws:
+                r.setdefault(w, (ord(w) - 0xE000) % 97)
+            tot = sum(map(r.__getitem__, ws))
+        return -0.37 * len(ws) - 0.011 * tot - (0.5 if bos else 0.0)
 
 
 # CPU port vs the reference itself on the same 8 container cores (tools/calibrate_cpu.py, committed
@@ -458,7 +472,7 @@ def main():
     # encoder, beam decode, the finished-hypothesis records to the host and the rescoring.
     lm_line = None
     if not args.no_configs:
-        from casr.results import records_by_utterance, second_pass_select
+        from casr.results import second_pass_arrays
         Bl, kl = args.config3_batch, 16
         eng5 = Engine(cfg, *synthetic_state_dicts(cfg, peaked=True), device=dev)
         eng5.set_precision(args.precision)
@@ -491,11 +505,11 @@ def main():
             ev.synchronize()
             # one sequential copy out of the pinned (possibly uncached) buffers, then the gathers
             toks, blen, steps, rt, rs, rv = (h.numpy().copy() for h in pinned[slot])
-            recs = records_by_utterance(rt, rs, rv)
             best = {b: (toks[b, :blen[b]].tolist(), 0.0) for b in range(Bl)}
-            best.update(second_pass_select(recs, i2w, lm, 1.5, 1.5))
+            best.update(second_pass_arrays(rt, rs, rv, i2w, lm, 1.5, 1.5))
             info["steps"] = int(steps[0])
-            info["rescored"] = sum(1 for v in recs.values() if len(v) > 1)
+            nrec = np.bincount(np.nonzero(rv)[0], minlength=Bl)
+            info["rescored"] = int(np.count_nonzero(nrec > 1))
             return best
 
         def run_lm(n):

@@ -124,3 +124,50 @@ def second_pass_select(records, int2word, lm_model, lm_weight, length_weight):
         comb = [s + lm_weight * q + length_weight * len(t) for (t, s), q in zip(v, lm)]
         out[b] = v[int(np.argmax(comb))]
     return out
+
+
+def _word_array(int2word, n):
+    """int2word as an object array over ids 0 .. n - 1 (the word strings themselves, not copies),
+    or None when the mapping does not cover that range."""
+    try:
+        return np.array([int2word[i] for i in range(n)] + [None], dtype=object)[:n]
+    except (KeyError, IndexError, TypeError):
+        return None
+
+
+def second_pass_arrays(rec_tokens, rec_score, rec_valid, int2word, lm_model, lm_weight, length_weight):
+    """second_pass_select(records_by_utterance(rec_tokens, rec_score, rec_valid), ...) from the record
+    arrays directly: the same choice per utterance with records (model.py:749-763) and the same
+    returned (tokens, logp), the LM called with the same sentences in the same order, but without
+    a Python token list per record (the words come from one object-array gather, and only the
+    chosen records become lists).  Falls back to the list form when int2word does not cover the
+    token ids."""
+    bs, ls, cs = np.nonzero(rec_valid)
+    if len(bs) == 0:
+        return {}
+    full = rec_tokens[bs, ls, cs]  # [n][L]: the records' token rows, in (utterance, step, rank) order
+    used = full[np.arange(full.shape[1])[None, :] < ls[:, None]]  # the l tokens of each step-l record
+    warr = _word_array(int2word, int(used.max()) + 1) if used.size else np.array([], dtype=object)
+    if warr is None or (used.size and int(used.min()) < 0):
+        return second_pass_select(records_by_utterance(rec_tokens, rec_score, rec_valid), int2word, lm_model,
+                                  lm_weight, length_weight)
+    full = np.where(np.arange(full.shape[1])[None, :] < ls[:, None], full, 0)  # (slots past l unused)
+    scores = rec_score[bs, ls, cs].tolist()
+    lens = ls.tolist()
+    starts = np.flatnonzero(np.r_[True, bs[1:] != bs[:-1]]).tolist() + [len(bs)]
+    words = None
+    out = {}
+    for a, z in zip(starts[:-1], starts[1:]):
+        b = int(bs[a])
+        if z - a == 1:
+            out[b] = (full[a, :lens[a]].tolist(), scores[a])
+            continue
+        if words is None:
+            words = warr[full] if len(warr) else np.empty(full.shape, dtype=object)
+        rows = words[a:z].tolist()
+        lm = [lm_model.score(' '.join(row[:l]), bos=True) for row, l in zip(rows, lens[a:z])]
+        comb = [sc + lm_weight * q + length_weight * l for sc, q, l in zip(scores[a:z], lm, lens[a:z])]
+        i = a + int(np.argmax(comb))
+        out[b] = (full[i, :lens[i]].tolist(), scores[i])
+    return out
+

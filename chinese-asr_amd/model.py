@@ -13,8 +13,7 @@ from gpd import gpd
 from casr.config import config_from_gpd
 from casr.engine import Engine
 from casr.lib import pack_weights
-from casr.results import (EvalOutput, get_wer, greedy_outputs, greedy_steps, records_by_utterance,
-                          second_pass_select)
+from casr.results import EvalOutput, get_wer, greedy_outputs, greedy_steps, second_pass_arrays
 from casr.vocab import load_vocab
 from casr.weights import check_state_dicts, load_checkpoint, save_checkpoint, synthetic_state_dicts
 
@@ -140,11 +139,10 @@ class Model(object):
         i2w = self._int2word(int2word)
         if second_pass:
             rt, rs, rv = (x.cpu().numpy() for x in self.engine.beam_records())
-            recs = records_by_utterance(rt, rs, rv)
-            if lm_model is None and any(len(v) > 1 for v in recs.values()):
+            if lm_model is None and bool((np.bincount(np.nonzero(rv)[0], minlength=bsz) > 1).any()):
                 # the reference calls lm_model.score here (model.py:755) and fails
                 raise AttributeError("second_pass=True needs lm_model ('NoneType' object has no attribute 'score')")
-            best.update(second_pass_select(recs, i2w, lm_model, lm_weight, length_weight))
+            best.update(second_pass_arrays(rt, rs, rv, i2w, lm_model, lm_weight, length_weight))
         pred_text = [''.join([i2w[idx] for idx in best[b][0]]) for b in range(bsz)]
         score = [best[b][1] for b in range(bsz)]
         if text is not None:

@@ -64,6 +64,30 @@ def test_second_pass_rule():
     assert sel[1] == recs[1][0]  # a single finished hypothesis is taken as is
 
 
+def test_second_pass_arrays_equals_record_lists():
+    """second_pass_arrays (bench config 5 and the drop-in Model's beam path) chooses the same record
+    per utterance and returns the same (tokens, logp) as second_pass_select over
+    records_by_utterance, on random records (padding slots past each record's length hold -1, as
+    the device leaves them), with no records, and with an int2word that does not cover the ids (the
+    list form then runs)."""
+    from casr.results import second_pass_arrays
+    i2w = pua_int2word(5004)
+    lm = StubLM()
+    rs_ = np.random.RandomState(3)
+    for B, L, k, p in ((16, 40, 16, 0.08), (8, 12, 4, 0.3), (4, 6, 2, 0.0)):
+        rv = (rs_.rand(B, L, k) < p).astype(np.uint8)
+        rt = np.full((B, L, k, L), -1, np.int32)
+        for b, l, c in zip(*np.nonzero(rv)):
+            rt[b, l, c, :l] = rs_.randint(0, 5004, size=l)
+        rsc = rs_.randn(B, L, k).astype(np.float32)
+        ref = second_pass_select(records_by_utterance(rt, rsc, rv), i2w, lm, 1.5, 1.5)
+        assert second_pass_arrays(rt, rsc, rv, i2w, lm, 1.5, 1.5) == ref
+        partial = {i: w for i, w in i2w.items() if i % 2}
+        if ref:
+            with pytest.raises(KeyError):  # the list form's lookup of a missing word, as the reference
+                second_pass_arrays(rt, rsc, rv, partial, lm, 1.5, 1.5)
+
+
 def test_wer():
     assert edit_distance("abc", "abc") == 0
     assert edit_distance("", "abc") == 3
