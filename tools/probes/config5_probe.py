@@ -14,7 +14,7 @@ import torch  # noqa: E402
 from bench import _StubLM, fbank_batch  # noqa: E402
 from casr.config import CasrConfig  # noqa: E402
 from casr.engine import Engine  # noqa: E402
-from casr.results import records_by_utterance, second_pass_select  # noqa: E402
+from casr.results import records_by_utterance, second_pass_arrays, second_pass_select  # noqa: E402
 from casr.weights import synthetic_state_dicts  # noqa: E402
 
 
@@ -67,8 +67,7 @@ def main():
         t1 = time.perf_counter()
         toks, blen, steps, rt, rs, rv = (h.numpy().copy() for h in pinned[slot])
         t2 = time.perf_counter()
-        recs = records_by_utterance(rt, rs, rv)
-        second_pass_select(recs, i2w, lm, 1.5, 1.5)
+        second_pass_arrays(rt, rs, rv, i2w, lm, 1.5, 1.5)
         t3 = time.perf_counter()
         print(f"pipe: enqueue {1e3 * te:.2f} ms, wait {1e3 * (t1 - t0):.2f}, copy-out {1e3 * (t2 - t1):.2f}, "
               f"host {1e3 * (t3 - t2):.2f} ms", flush=True)
