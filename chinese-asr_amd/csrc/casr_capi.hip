@@ -174,7 +174,11 @@ struct casr_handle {
   bool s16_valid = false;           // the bound blob's s16 images are usable (Layout::info)
   bool proj_small = false;          // every |W_p| < 16 (Layout::info + 4)
   bool dec_small = false;           // every decoder LSTM weight < 16 (Layout::info + 5)
-  DevBuf x16;                       // s16 row image of the current layer input [B*Tp][Kp]
+  DevBuf x16;                       // s16 image of the current layer input [B*Tp][Kp] (or 16-k-block major)
+  // the encoder layers' W_ih s16 images 16-k-block major (CASR_OPT_X16_KM), built at bind from an
+  // s16-valid blob: layer l at wih16km_off[l]
+  DevBuf wih16km;
+  size_t wih16km_off[CASR_MAX_LAYERS] = {};
   // folded greedy decode (CASR_OPT_DEC_FOLD): fused projection | LSTM-gate fragment image and the
   // per-token gate table, built at bind from an s16-valid blob; the gates buffer [R][4 HD]
   DevBuf wfold, egates, fgates, wq16;
@@ -478,6 +482,18 @@ int casr_bind_weights(casr_handle* h, const float* packed_device) {
     HIP_OK(h, hipStreamSynchronize(nullptr));
     h->fold_ready = h->s16_valid;
   }
+  if (h->s16_valid) {  // 16-k-block-major copies of the input-projection weight images
+    size_t tot = 0;
+    for (int l = 0; l < h->cfg.enc_layers; ++l) {
+      h->wih16km_off[l] = tot;
+      tot += (size_t)8 * H * s16_kpad(l == 0 ? D : C);
+    }
+    HIP_OK(h, h->wih16km.ensure(tot * sizeof(float)));
+    for (int l = 0; l < h->cfg.enc_layers; ++l)
+      HIP_OK(h, launch_relayout_km16(h->W + h->L.enc_wih16[l], 8 * H, s16_kpad(l == 0 ? D : C),
+                                     h->wih16km.as<float>() + h->wih16km_off[l], nullptr));
+    HIP_OK(h, hipStreamSynchronize(nullptr));
+  }
   return CASR_OK;
 }
 
@@ -523,7 +539,7 @@ void casr_destroy(casr_handle* h) {
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->gflags, &h->fe_const,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout, &h->wfold, &h->wfold32, &h->coldbuf,
-                    &h->egates, &h->fgates, &h->wq16})
+                    &h->egates, &h->fgates, &h->wq16, &h->wih16km})
     b->release();
   delete h;
 }
@@ -557,8 +573,8 @@ int casr_recurrence_mode(const casr_handle* h, int B) {
 int casr_set_option(casr_handle* h, int option, int value) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
-  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 2, 2, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1, 1, 1};
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 2, 2, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1, 1, 1, 1};
   if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
     return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
   if (value < lo[option] || value > hi[option])
@@ -668,6 +684,8 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
     HIP_OK(h, fill_multi(fl, s));
   }
   const bool s16 = h->s16();
+  // the layer-input images 16-k-block major (CASR_OPT_X16_KM and the GEMM / keys forms that read them)
+  const int km = s16 && x16_km(h->tune) ? 1 : 0;
   if (s16) HIP_OK(h, h->x16.ensure(rows * s16_kpad(D) * sizeof(float)));
   if (persistent) HIP_OK(h, h->hx.ensure(rec_layer_granule_bytes(B, layout)));
   const int32_t* dl = h->lens.as<int32_t>();
@@ -679,7 +697,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
     if (s16 && features_x16_supported(T)) {
       HIP_OK(h, launch_features_x16(fb, frames, B, T, eps, h->lens.as<int32_t>(), h->fstat.as<float>(),
                                     h->x16.as<uint16_t>(), s16_kpad(D),
-                                    eflag, s));
+                                    eflag, s, km));
       x16_ready = true;  // feat stays NULL: layer 0 reads only the image (no residual input)
     } else {
       HIP_OK(h, h->feat.ensure(rows * D * sizeof(float)));
@@ -699,10 +717,11 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
     if (s16) {
       const int kp = s16_kpad(din);
       if (!x16_ready)
-        HIP_OK(h, launch_split_rows(x, din, (int)rows, din, kp, h->x16.as<uint16_t>(), eflag, s));
-      HIP_OK(h, launch_input_proj_s16_big(h->x16.as<float>(), (int)rows, kp, h->W + h->L.enc_wih16[l],
+        HIP_OK(h, launch_split_rows(x, din, (int)rows, din, kp, h->x16.as<uint16_t>(), eflag, s, km));
+      HIP_OK(h, launch_input_proj_s16_big(h->x16.as<float>(), (int)rows, kp,
+                                          km ? h->wih16km.as<float>() + h->wih16km_off[l] : h->W + h->L.enc_wih16[l],
                                           h->W + h->L.enc_bias[l], h->gin.as<float>(), s, din,
-                                          h->tune[CASR_OPT_GEMM16_PERSIST], h->tune[CASR_OPT_GEMM16_TAIL]));
+                                          h->tune[CASR_OPT_GEMM16_PERSIST], h->tune[CASR_OPT_GEMM16_TAIL], km));
     } else {
       HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
                                   h->gin.as<float>(), s));
@@ -733,7 +752,7 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
         uint16_t* x16o = s16 ? h->x16.as<uint16_t>() : nullptr;
         er = launch_rec_layer(whh, h->gin.as<float>(), xin, out, x16o, reinterpret_cast<uint32_t*>(h->hx.p),
                               h->hfin.as<float>(), h->cst.as<float>(), dl, B, Tp, residual, s16,
-                              eflag, tbuf.as<uint32_t>(), layout, h->tune, s);
+                              eflag, tbuf.as<uint32_t>(), layout, h->tune, s, km);
       }
       if (er == hipErrorCooperativeLaunchTooLarge) {
         // the device cannot hold the whole grid at once (e.g. CUs taken by other work): this layer
@@ -808,12 +827,12 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
   // s16x3 keys on every s16 path (the per-step fallback splits the encoder output first), so both
   // recurrences give the same keys bits
   if (s16 && !x16_ready) {
-    HIP_OK(h, launch_split_rows(h->enc_out, C, (int)rows, C, C, h->x16.as<uint16_t>(), eflag, s));
+    HIP_OK(h, launch_split_rows(h->enc_out, C, (int)rows, C, C, h->x16.as<uint16_t>(), eflag, s, km));
     x16_ready = true;
   }
   if (x16_ready)  // s16x3 keys from the image the last persistent layer wrote
     HIP_OK(h, launch_keys_s16(h->x16.as<float>(), B, Tp, h->W + h->L.wenc16, h->W + h->L.b_attn,
-                              h->keysT.as<float>(), s, h->tune[CASR_OPT_KEYS_ROWS]));
+                              h->keysT.as<float>(), s, h->tune[CASR_OPT_KEYS_ROWS], km));
   else
     HIP_OK(h, launch_keys(h->enc_out, B, Tp, h->W + h->L.wencT, h->W + h->L.b_attn, h->keysT.as<float>(), s));
   }

@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 2, 0, 0, 1, 0, 0, 1, 1};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -223,7 +223,8 @@ hipError_t launch_log_mel(const float* wav, const int32_t* nsamp, int B, int Nma
 bool features_x16_supported(int T);
 // stats: [B][2][D] floats of scratch (per-utterance mean and std + eps of the 720 dimensions)
 hipError_t launch_features_x16(const float* fbank, const int32_t* frames, int B, int T, float eps,
-                               int32_t* feat_len, float* stats, uint16_t* x16, int Kp, int32_t* err, hipStream_t s);
+                               int32_t* feat_len, float* stats, uint16_t* x16, int Kp, int32_t* err, hipStream_t s,
+                               int km = 0);
 hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int T, float eps,
                            float* feat, int32_t* feat_len, float* stats, hipStream_t s);
 hipError_t launch_gather_utts(const float* const* ptrs, const int32_t* lens, int B, int Tp,
@@ -232,13 +233,25 @@ hipError_t launch_gather_utts(const float* const* ptrs, const int32_t* lens, int
 // encoder.hip
 hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, const float* bias,
                              float* Gin, hipStream_t s);
-// gemm16.hip: the s16x3 input projection on 256 x 256 tiles; X16 / W16 are s16 row images with Kp
-// (multiple of 64) k per row.  K: the real input width (the images are zero from K to Kp); 0 = Kp.
-// persist / tail: CASR_OPT_GEMM16_PERSIST / CASR_OPT_GEMM16_TAIL
+// s16 images of an activation or weight matrix with rows R and Kp (multiple of 64) k per row, in one
+// of two layouts (the same words): the row image [R][Kp / 32][32 hi | 32 lo] halves, or (km, round
+// 5, CASR_OPT_X16_KM) 16-k-block major [Kp / 16][R][16 hi | 16 lo], in which 16 consecutive rows of
+// one 16-k block are 1 KB contiguous (whole 128-B lines for the input GEMM's 16-deep stages).
+// x16_km: whether one encode uses the 16-k-major layout (the ping-pong input GEMM, the balanced tail
+// and the row-streaming keys form read it; the other forms take row images)
+inline bool x16_km(const Tuning& t) {
+  return t[CASR_OPT_X16_KM] && t[CASR_OPT_GEMM16_PERSIST] == 2 && t[CASR_OPT_GEMM16_TAIL] != 1 &&
+         t[CASR_OPT_KEYS_ROWS];
+}
+// gemm16.hip: the s16x3 input projection on 256 x 256 tiles; X16 / W16 are s16 images with Kp
+// (multiple of 64) k per row (km: both 16-k-block major, X16 with M rows).  K: the real input width
+// (the images are zero from K to Kp); 0 = Kp.  persist / tail: CASR_OPT_GEMM16_PERSIST / _TAIL
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                     float* Gin, hipStream_t s, int K, int persist, int tail);
+                                     float* Gin, hipStream_t s, int K, int persist, int tail, int km = 0);
+// a row-image weight matrix [R][Kp] -> its 16-k-block-major image (bind time)
+hipError_t launch_relayout_km16(const float* rowimg, int R, int Kp, float* km, hipStream_t s);
 hipError_t launch_split_rows(const float* X, int ldx, int M, int K, int Kp, uint16_t* out, int32_t* err,
-                             hipStream_t s);
+                             hipStream_t s, int km = 0);
 inline int s16_kpad(int K) { return (K + 63) / 64 * 64; }  // even number of 32-k tiles (gemm16.hip)
 hipError_t launch_rec_step(const float* Whh_f, const float* Gin, const float* xin, float* out,
                            const float* hprev, float* hnext, float* cst, float* hfin,
@@ -260,9 +273,10 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, int layout, hipStream_t s);  // 
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int s16, int32_t* err, uint32_t* trace, int layout, const Tuning& t,
-                            hipStream_t s);
+                            hipStream_t s, int km = 0);
+// enc16: the encoder output's s16 image (km: 16-k-block major; rows = 1 only)
 hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc16, const float* b_attn,
-                           float* keysT, hipStream_t s, int rows = 1);
+                           float* keysT, hipStream_t s, int rows = 1, int km = 0);
 hipError_t launch_keys(const float* enc, int B, int Tp, const float* wencT, const float* b_attn,
                        float* keysT, hipStream_t s);
 

@@ -350,7 +350,7 @@ hipError_t launch_input_proj(const float* X, int M, int Din, const float* W, con
 // element beyond the f16 range (its hi would be infinite).
 __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ X, int ldx, int M, int K,
                                                          int Kp, uint16_t* __restrict__ out,
-                                                         int32_t* __restrict__ err) {
+                                                         int32_t* __restrict__ err, int km) {
   const int ng = Kp / 8;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (size_t)M * ng) return;
@@ -375,17 +375,18 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
     lv[e / 2] = __builtin_amdgcn_perm(w1, w0, 0x07060302u);
   }
   if (!range_ok) __hip_atomic_fetch_or(err, CASR_DEV_F16_RANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint16_t* op = out + (size_t)row * Kp * 2 + (k0 / 32) * 64 + (k0 % 32);
+  // row image [M][Kp / 32][32 hi | 32 lo], or (km) 16-k-block major [Kp / 16][M][16 hi | 16 lo]
+  uint16_t* op = km ? out + ((size_t)(k0 / 16) * M + row) * 32 + (k0 % 16) : out + (size_t)row * Kp * 2 + (k0 / 32) * 64 + (k0 % 32);
   *reinterpret_cast<u32x4*>(op) = hv;
-  *reinterpret_cast<u32x4*>(op + 32) = lv;
+  *reinterpret_cast<u32x4*>(op + (km ? 16 : 32)) = lv;
 }
 
 hipError_t launch_split_rows(const float* X, int ldx, int M, int K, int Kp, uint16_t* out, int32_t* err,
-                             hipStream_t s) {
+                             hipStream_t s, int km) {
   if (M <= 0 || Kp % 32 != 0 || K > Kp) return hipErrorInvalidValue;
   const size_t n = (size_t)M * (Kp / 8);
   hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, X, ldx, M, K, Kp, out,
-                     err);
+                     err, km);
   return hipGetLastError();
 }
 
@@ -432,7 +433,7 @@ constexpr int KR_NBUF = 4;                 // ring slots (three items in flight)
 
 __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict__ enc16, const float* __restrict__ w16,
                                                         const float* __restrict__ bias, float* __restrict__ keysT,
-                                                        int B, int Tp, int Tq) {
+                                                        int B, int Tp, int Tq, int km) {
   __shared__ __attribute__((aligned(16))) float ring[KR_NBUF * KR_IF];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
   const int ng = (Tp + KR_G - 1) / KR_G, NI = B * ng, G = gridDim.x;
@@ -454,7 +455,9 @@ __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict_
     b = x / ng;
     j = x - b * ng;
   };
-  // 32 DMA instructions of 1 KB per item (k-tile kt, rows 8 h .. 8 h + 7), four per wave
+  // 32 DMA instructions of 1 KB per item (k-tile kt, rows 8 h .. 8 h + 7), four per wave.  km:
+  // chunk c of a row's 32-k tile kt is sub-chunk (c & 1) + 2 (c >> 2) of 16-k block 2 kt + ((c >> 1) & 1)
+  const size_t Mimg = (size_t)B * Tp;
   auto stage = [&](int q) {
     int b, j;
     item(q, b, j);
@@ -464,7 +467,10 @@ __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict_
       const int i = w + 8 * u, kt = i >> 1, h = i & 1;
       const int row = 8 * h + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
       const int t = min(KR_G * j + row, Tp - 1);
-      if (!(CASR_KR_DIAG & 1)) lds_dma16(enc16 + ((size_t)b * Tp + t) * C + kt * 32 + 4 * c, dst + (kt * KR_G + 8 * h) * 32);
+      const size_t gr = (size_t)b * Tp + t;
+      const float* src = km ? enc16 + ((size_t)(2 * kt + ((c >> 1) & 1)) * Mimg + gr) * 16 + 4 * ((c & 1) + 2 * (c >> 2))
+                            : enc16 + gr * C + kt * 32 + 4 * c;
+      if (!(CASR_KR_DIAG & 1)) lds_dma16(src, dst + (kt * KR_G + 8 * h) * 32);
     }
   };
   // VMEM operations this wave issued after the DMA of item q, at the top of iteration q: each
@@ -530,9 +536,9 @@ __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict_
 // keys from the s16 row image of the encoder output (written by the last persistent layer) and
 // of wencT: s16x3 products, same KeysEpi store (rows = 1: keys16_kernel, the default)
 hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc16, const float* b_attn,
-                           float* keysT, hipStream_t s, int rows) {
+                           float* keysT, hipStream_t s, int rows, int km) {
   const int M = B * Tp;
-  if (M <= 0 || C % GB_K != 0) return hipErrorInvalidValue;
+  if (M <= 0 || C % GB_K != 0 || (km && !rows)) return hipErrorInvalidValue;
   if (rows) {
     static int ncu = [] {
       int dev = 0, v = 0;
@@ -543,7 +549,7 @@ hipError_t launch_keys_s16(const float* enc16, int B, int Tp, const float* wenc1
     const int Tq = (Tp + 3) & ~3, NI = B * ((Tp + KR_G - 1) / KR_G);
     if ((size_t)2 * B * A * Tq * 4 >= 0xFFFFFFF0u) return hipErrorInvalidValue;  // 32-bit buffer offsets
     hipLaunchKernelGGL(keys16_kernel, dim3(std::min(NI, ncu)), dim3(512), 0, s, enc16, wenc16, b_attn, keysT, B, Tp,
-                       Tq);
+                       Tq, km);
     return hipGetLastError();
   }
   KeysEpi epi{keysT, b_attn, Tp, (Tp + 3) & ~3, B};

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(RTH) void features_rows_kernel(const float* __restr
                                                             const int32_t* __restrict__ frames, int T, int Tp,
                                                             const float* __restrict__ stats, float* __restrict__ feat,
                                                             uint32_t* __restrict__ x16, int Kp,
-                                                            int32_t* __restrict__ err) {
+                                                            int32_t* __restrict__ err, int km) {
   __shared__ __attribute__((aligned(16))) float xs[RNF * F];  // frames 3 j0 - 4 .. 3 (j0 + RJ) + 3
   const int b = blockIdx.y, j0 = blockIdx.x * RJ, p = threadIdx.x;
   const int nf = min(max(frames[b], 0), T), lp = nf / 3;
@@ -327,9 +327,11 @@ __global__ __launch_bounds__(RTH) void features_rows_kernel(const float* __restr
     }
     if constexpr (X16) {
       const uint32_t w0 = split16_word(v.x), w1 = split16_word(v.y);
-      uint32_t* row = x16 + ((size_t)b * Tp + j) * Kp + (o0 >> 5) * 32 + ((o0 & 31) >> 1);
-      row[0] = (w0 & 0xFFFFu) | (w1 << 16);            // hi halves of columns o0, o0 + 1
-      row[16] = (w0 >> 16) | (w1 & 0xFFFF0000u);      // lo halves
+      // row image: 32-k tiles [32 hi | 32 lo] halves; km: 16-k-block major [Kp / 16][B Tp][16 hi | 16 lo]
+      uint32_t* row = km ? x16 + ((size_t)(o0 >> 4) * gridDim.y * Tp + (size_t)b * Tp + j) * 16 + ((o0 & 15) >> 1)
+                         : x16 + ((size_t)b * Tp + j) * Kp + (o0 >> 5) * 32 + ((o0 & 31) >> 1);
+      row[0] = (w0 & 0xFFFFu) | (w1 << 16);               // hi halves of columns o0, o0 + 1
+      row[km ? 8 : 16] = (w0 >> 16) | (w1 & 0xFFFF0000u);  // lo halves
       const float ax = fabsf(v.x), ay = fabsf(v.y);
       range_ok &= !(ax >= 65520.f && ax < INFINITY) && !(ay >= 65520.f && ay < INFINITY);
     } else {
@@ -355,7 +357,7 @@ hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int
     hipLaunchKernelGGL(features_stats_kernel, dim3((F / SM) * ((B + 7) / 8 * 8)), dim3(SRM * SPH), shm, s, fbank, frames, B, T, eps, stats,
                        feat_len);
     hipLaunchKernelGGL(features_rows_kernel<false>, dim3((Tp + RJ - 1) / RJ, B), dim3(RTH), 0, s, fbank, frames, T, Tp,
-                       eps >= 0.f ? stats : nullptr, feat, nullptr, 0, nullptr);
+                       eps >= 0.f ? stats : nullptr, feat, nullptr, 0, nullptr, 0);
     return hipGetLastError();
   }
   // longer utterances: the two-pass kernels
@@ -369,14 +371,15 @@ hipError_t launch_features(const float* fbank, const int32_t* frames, int B, int
 bool features_x16_supported(int T) { return T / 3 > 0 && T <= FS_MAX_T; }
 
 hipError_t launch_features_x16(const float* fbank, const int32_t* frames, int B, int T, float eps,
-                               int32_t* feat_len, float* stats, uint16_t* x16, int Kp, int32_t* err, hipStream_t s) {
+                               int32_t* feat_len, float* stats, uint16_t* x16, int Kp, int32_t* err, hipStream_t s,
+                               int km) {
   const int Tp = T / 3;
   if (B <= 0 || !features_x16_supported(T) || Kp != 2 * RTH) return hipErrorInvalidValue;
   const size_t shm = (size_t)(T + FS_PAD + FS_PAD2) * SM * sizeof(float);
   hipLaunchKernelGGL(features_stats_kernel, dim3((F / SM) * ((B + 7) / 8 * 8)), dim3(SRM * SPH), shm, s, fbank, frames, B, T, eps, stats,
                      feat_len);
   hipLaunchKernelGGL(features_rows_kernel<true>, dim3((Tp + RJ - 1) / RJ, B), dim3(RTH), 0, s, fbank, frames, T, Tp,
-                     eps >= 0.f ? stats : nullptr, nullptr, reinterpret_cast<uint32_t*>(x16), Kp, err);
+                     eps >= 0.f ? stats : nullptr, nullptr, reinterpret_cast<uint32_t*>(x16), Kp, err, km);
   return hipGetLastError();
 }
 

@@ -639,10 +639,12 @@ __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restri
 // counted vmcnt waits and a raw s_barrier per stage.  The MFMAs per accumulator are compute() of
 // gemm16_bias_kernel (same fragments, order and 2^11 scaling), and the epilogue its slab form: the
 // same bits.
+// km: A (rows r0 .. r0 + M - 1 of an Mimg-row image) and W 16-k-block major; else row images (A16 at
+// row r0 already)
 template <int RT>
 __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
                                                              const float* __restrict__ bias, float* __restrict__ Cout,
-                                                             int M, int N, int Kp) {
+                                                             int M, int N, int Kp, int km, int r0, int Mimg) {
   constexpr int BM = 32 * RT, BN = 128, ROWS = BM + BN, STF = ROWS * G16_K;  // floats per stage
   constexpr int NBUF = 4, NI = ROWS / 8, PW = (NI + 3) / 4;  // DMA instructions per stage / per wave
   static_assert(NBUF * STF * 4 <= 160 * 1024 && (NBUF - 2) * PW < 64, "ring fits the LDS; vmcnt range");
@@ -664,8 +666,14 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
       const int i = wave + 4 * j;
       if (i < NI) {
         const int row = 8 * i + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
-        const float* src = row < BM ? A16 + (size_t)min(m0 + row, M - 1) * Kp + k0 + 4 * c
-                                    : W16 + (size_t)(n0 + row - BM) * Kp + k0 + 4 * c;
+        const int ar = min(m0 + row, M - 1), wr = n0 + row - BM;
+        const float* src;
+        if (km) {  // chunk c of the 32-k tile: sub-chunk (c & 1) + 2 (c >> 2) of 16-k block 2 kt + ((c >> 1) & 1)
+          const size_t blk = (size_t)(2 * kt + ((c >> 1) & 1)), sub = 4 * ((c & 1) + 2 * (c >> 2));
+          src = row < BM ? A16 + (blk * Mimg + r0 + ar) * 16 + sub : W16 + (blk * N + wr) * 16 + sub;
+        } else {
+          src = row < BM ? A16 + (size_t)ar * Kp + k0 + 4 * c : W16 + (size_t)wr * Kp + k0 + 4 * c;
+        }
         lds_dma16(src, dst + 8 * i * G16_K);
       }
     }
@@ -707,7 +715,7 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
   }
   // epilogue: RT 32-row slabs through the ring, stored as 512-B row segments (+ bias)
   constexpr int LDC = BN + 4;
-  const int c4 = tid & 31, r0 = tid >> 5;  // 32 float4 per row, 8 rows per pass
+  const int c4 = tid & 31, rp = tid >> 5;  // 32 float4 per row, 8 rows per pass
   const float4 b4 = *reinterpret_cast<const float4*>(bias + n0 + c4 * 4);
 #pragma unroll
   for (int tm = 0; tm < RT; ++tm) {
@@ -717,7 +725,7 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
       ring[((e & 3) + 8 * (e >> 2) + 4 * hsel) * LDC + wave * 32 + r32] = acc[tm][e] * S16_LO_INV;
     __syncthreads();
 #pragma unroll
-    for (int row = r0; row < 32; row += 8) {
+    for (int row = rp; row < 32; row += 8) {
       const int gr = m0 + tm * 32 + row;
       if (gr < M) {
         const float4 v = *reinterpret_cast<const float4*>(ring + row * LDC + c4 * 4);
@@ -728,21 +736,20 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
   }
 }
 
-// tail rows [r0, M) of the input projection as gemm16_tail_kernel tiles: false when they do not fit
-// one round of ncu workgroups (the caller then takes the half-tile launch)
+// tail rows [r0, M) of the input projection as gemm16_tail_kernel tiles (one round of ncu workgroups
+// while the rows allow RT <= 5)
 static bool launch_tail_balanced(const float* A16, const float* W16, const float* bias, float* Gin, int Mt, int N, int Kp,
-                                 int ncu, hipStream_t s) {
+                                 int ncu, hipStream_t s, int km, int r0, int Mimg) {
   if (Mt <= 0 || N % 128 != 0) return false;
   const int units = (Mt + 31) / 32 * (N / 128);
-  const int RT = (units + ncu - 1) / ncu;
-  if (RT > 5) return false;
+  const int RT = std::min(5, (units + ncu - 1) / ncu);  // (past 5 x ncu units: more than one round)
   const int blocks = (Mt + 32 * RT - 1) / (32 * RT) * (N / 128);
   switch (RT) {
-    case 1: hipLaunchKernelGGL(gemm16_tail_kernel<1>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
-    case 2: hipLaunchKernelGGL(gemm16_tail_kernel<2>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
-    case 3: hipLaunchKernelGGL(gemm16_tail_kernel<3>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
-    case 4: hipLaunchKernelGGL(gemm16_tail_kernel<4>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
-    default: hipLaunchKernelGGL(gemm16_tail_kernel<5>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp); break;
+    case 1: hipLaunchKernelGGL(gemm16_tail_kernel<1>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
+    case 2: hipLaunchKernelGGL(gemm16_tail_kernel<2>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
+    case 3: hipLaunchKernelGGL(gemm16_tail_kernel<3>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
+    case 4: hipLaunchKernelGGL(gemm16_tail_kernel<4>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
+    default: hipLaunchKernelGGL(gemm16_tail_kernel<5>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
   }
   return true;
 }
@@ -750,8 +757,9 @@ static bool launch_tail_balanced(const float* A16, const float* W16, const float
 }  // namespace
 
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                     float* Gin, hipStream_t s, int K, int persist, int tail) {
+                                     float* Gin, hipStream_t s, int K, int persist, int tail, int km) {
   const int N = 8 * H;
+  if (km && (persist != 2 || tail == 1)) return hipErrorInvalidValue;  // the forms that read 16-k-major images
   if (Kp % (2 * G16_K) != 0 || M <= 0 || N % G16_N != 0) return hipErrorInvalidValue;
   const int NB = N / G16_N, NM = (M + G16_M - 1) / G16_M;
   // smallest group count whose W share (NB/NG slices of 256 rows x Kp words) fits 3/4 of an L2
@@ -786,8 +794,12 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     const int Mm = std::min(M, NMm * G16_M);
     if (persist == 2) {  // ping-pong form: 16-deep stages
       const int nk16 = (K > 0 && K <= Kp ? K + 15 : Kp) / 16;
-      hipLaunchKernelGGL((gemm16_pp_kernel<0, 1>), dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
-                         N, Kp, om, total, nk16, M);
+      if (km)
+        hipLaunchKernelGGL((gemm16_pp_kernel<0, 1, 0, 0, true>), dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias,
+                           Gin, Mm, N, Kp, om, total, nk16, M);
+      else
+        hipLaunchKernelGGL((gemm16_pp_kernel<0, 1>), dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
+                           N, Kp, om, total, nk16, M);
     } else {
       hipLaunchKernelGGL(gemm16_persist_kernel<0>, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm,
                          N, Kp, om, total, nk);
@@ -795,7 +807,8 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     if (NMm < NM) {
       const size_t r0 = (size_t)NMm * G16_M;
       const int Mt = M - (int)r0, NMt = (Mt + 127) / 128;
-      if (tail == 2 && launch_tail_balanced(X16 + r0 * Kp, W16, bias, Gin + r0 * N, Mt, N, Kp, ncu, s))
+      if (tail == 2 && launch_tail_balanced(km ? X16 : X16 + r0 * Kp, W16, bias, Gin + r0 * N, Mt, N, Kp, ncu, s, km,
+                                            (int)r0, M))
         return hipGetLastError();
       const Order16 ot{NB, NMt, NG};  // XCD grouping of the tail: the same column slices per XCD
       hipLaunchKernelGGL((gemm16_bias_kernel<4, 1>), dim3(ot.blocks()), dim3(256), 0, s, X16 + r0 * Kp, W16, bias,
@@ -805,6 +818,30 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     hipLaunchKernelGGL(gemm16_bias_kernel<4>, dim3(order.blocks()), dim3(512), 0, s, X16, W16, bias, Gin, M, N, Kp,
                        order);
   }
+  return hipGetLastError();
+}
+
+// row image [R][Kp / 32][32 hi | 32 lo] halves -> 16-k-block major [Kp / 16][R][16 hi | 16 lo]: one
+// thread per (row, 16-k block), 64 B read as two 32-B halves of the row's 128-B tile, 64 B written
+__global__ void relayout_km16_kernel(const uint32_t* __restrict__ src, int R, int Kp, uint32_t* __restrict__ dst) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = Kp / 16;
+  if (i >= (size_t)R * nb) return;
+  const int r = (int)(i / nb), kb = (int)(i - (size_t)r * nb);
+  const uint32_t* t = src + (size_t)r * Kp + (kb >> 1) * 32 + (kb & 1) * 8;  // hi words of the block
+  uint32_t* o = dst + ((size_t)kb * R + r) * 16;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o[e] = t[e];           // hi halves
+    o[8 + e] = t[16 + e];  // lo halves
+  }
+}
+
+hipError_t launch_relayout_km16(const float* rowimg, int R, int Kp, float* km, hipStream_t s) {
+  if (R <= 0 || Kp % 32 != 0) return hipErrorInvalidValue;
+  const size_t n = (size_t)R * (Kp / 16);
+  hipLaunchKernelGGL(relayout_km16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     reinterpret_cast<const uint32_t*>(rowimg), R, Kp, reinterpret_cast<uint32_t*>(km));
   return hipGetLastError();
 }
 

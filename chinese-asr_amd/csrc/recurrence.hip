@@ -87,7 +87,7 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     float* __restrict__ out, uint16_t* __restrict__ x16, uint32_t* __restrict__ hx, float* __restrict__ hfin,
     float* __restrict__ cst, const int32_t* __restrict__ lens, int B, int Bp, int Tp, int residual,
     int32_t* __restrict__ err, uint32_t* __restrict__ trace, int nrg, int pre_sleep, int poll_gap,
-    int store_plain) {
+    int store_plain, int km) {
   constexpr int NW = RG * UW / 64;      // waves: 4 k-chunks x RG/16 row halves x UW/16 unit halves
   __shared__ f32x4 red[2][NW][4][64];  // double-buffered k-chunk partials
   __shared__ int s_tmax, s_quit[2];  // quit flag per step parity (read after the step's barrier)
@@ -122,7 +122,12 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
   const int U = ub * UW + u;
   const size_t si = ((size_t)d * B + b) * H + U;       // hfin / cst index (valid when b < B)
   const size_t gi = ((size_t)d * Bp + b) * H + U;      // granule index within a buffer
-  const int x16_col = ((d * H + U) >> 5) * 64 + ((d * H + U) & 31);  // s16 image column of (d, U)
+  // s16 image position of (d, U) in halves: row image rows of 2 C halves, column (d H + U) in 32-k tiles
+  // [32 hi | 32 lo]; km: 16-k-block major [C / 16][B Tp][16 hi | 16 lo] (lo 16 halves after hi)
+  const int xcol = d * H + U;
+  const size_t x16_base = km ? (size_t)(xcol >> 4) * B * Tp * 32 + (xcol & 15) : (size_t)((xcol >> 5) * 64 + (xcol & 31));
+  const size_t x16_rs = km ? 32 : 2 * C;  // halves per image row
+  const int x16_lo = km ? 16 : 32;
   __shared__ int s_plain;
   if (tid == 0) {
     s_tmax = 0;
@@ -349,9 +354,9 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
       // s16x3: the next layer's input row image, written here instead of by split_rows_kernel
       if (S16 && x16) {
         const uint32_t wv = split16_word(y);
-        uint16_t* xp = x16 + ((size_t)b * Tp + t) * (2 * C) + x16_col;
+        uint16_t* xp = x16 + ((size_t)b * Tp + t) * x16_rs + x16_base;
         xp[0] = (uint16_t)wv;
-        xp[32] = (uint16_t)(wv >> 16);
+        xp[x16_lo] = (uint16_t)(wv >> 16);
         const float m = fabsf(y);
         if (m >= 65520.f && m < INFINITY)
           __hip_atomic_fetch_or(err, CASR_DEV_F16_RANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -378,9 +383,9 @@ __global__ __launch_bounds__(RG * UW, 2) void rec_layer_kernel(
     for (int t = len; t < Tp; ++t) {
       out[((size_t)b * Tp + t) * C + d * H + U] = 0.f;
       if (S16 && x16) {
-        uint16_t* xp = x16 + ((size_t)b * Tp + t) * (2 * C) + x16_col;
+        uint16_t* xp = x16 + ((size_t)b * Tp + t) * x16_rs + x16_base;
         xp[0] = 0;
-        xp[32] = 0;
+        xp[x16_lo] = 0;
       }
     }
 }
@@ -469,7 +474,7 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, int layout, hipStream_t s) {
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int s16, int32_t* err, uint32_t* trace, int layout, const Tuning& t,
-                            hipStream_t s) {
+                            hipStream_t s, int km) {
   int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for every layout
   const int RG = rec_rows(layout), UW = rec_units(layout);
   int nrg = (B + RG - 1) / RG;
@@ -481,11 +486,11 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
     if (t[CASR_OPT_REC_COOP]) {
       // every workgroup co-resident or an immediate launch error (the hand-off spins need all of them)
       void* args[] = {&Whh_f, &Gin, &xin, &out, &x16, &hx, &hfin, &cst, &lens, &B, &Bp, &Tp, &residual,
-                      &err, &trace, &nrg, &sleep, &gap, &plain};
+                      &err, &trace, &nrg, &sleep, &gap, &plain, &km};
       return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kern), grid, block, args, 0, s);
     }
     hipLaunchKernelGGL(kern, grid, block, 0, s, Whh_f, Gin, xin, out, x16, hx, hfin, cst, lens, B, Bp, Tp, residual,
-                       err, trace, nrg, sleep, gap, plain);
+                       err, trace, nrg, sleep, gap, plain, km);
     return hipGetLastError();
   };
   switch (layout) {

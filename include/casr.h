@@ -244,6 +244,11 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            items of the encoder output through LDS, one workgroup per CU (default,
  *                            round 5); 0: 128 x 128 tiles (gemm_nt_kernel).  The same MFMAs in the
  *                            same order
+ *   CASR_OPT_X16_KM          1: the s16 images of the encoder's layer inputs (and of W_ih) are laid
+ *                            out 16-k-block major, so the input GEMM's 16-deep stages read whole
+ *                            cache lines (default, round 5; in effect with GEMM16_PERSIST = 2,
+ *                            GEMM16_TAIL != 1 and KEYS_ROWS = 1, the forms that read it); 0: row
+ *                            images.  The same words in another order: the same bits
  * Two options select numerics variants instead (the same token ids, floating-point results within
  * the stated tolerances, not bit for bit; tests/test_gpu_parity.py compares each pair):
  *   CASR_OPT_ATTN_DIRECT     0: attention scores in the split exponential form 1 - 2 / (1 + e^{2k}
@@ -296,7 +301,8 @@ enum {
   CASR_OPT_DIAG_COLD = 12,
   CASR_OPT_LOGMEL_Q16 = 13,
   CASR_OPT_KEYS_ROWS = 14,
-  CASR_OPT_COUNT = 15
+  CASR_OPT_X16_KM = 15,
+  CASR_OPT_COUNT = 16
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

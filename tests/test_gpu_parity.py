@@ -778,7 +778,10 @@ def test_input_gemm_tail_split_bitwise(eng, B):
     stages, two staggered wave groups, buffer stores that drop rows past M) with and without the
     tail split, against the round-2 persistent kernel and the per-tile kernel; and the balanced tail
     (CASR_OPT_GEMM16_TAIL = 2, the default: one round of 160 x 128 tiles at B = 256, 96 x 128 at
-    B = 128) against the half tiles."""
+    B = 128) against the half tiles; and the layer-input / W_ih images 16-k-block major
+    (CASR_OPT_X16_KM = 1, the default with those forms: written by the feature kernel, the recurrence
+    and split_rows, read by the ping-pong kernel, the balanced tail and the keys form) against row
+    images."""
     if eng.precision() != "s16x3":
         pytest.skip("the split-f16 input GEMM only")
     bind(eng, "peaked")
@@ -787,15 +790,18 @@ def test_input_gemm_tail_split_bitwise(eng, B):
     fb, fr = batch_fbank(frames, eng.device)
     outs = []
     try:
-        for tail, persist in ((2, 2), (1, 2), (0, 2), (2, 1), (1, 1), (0, 1), (1, 0)):
+        for tail, persist, km in ((2, 2, 1), (2, 2, 0), (0, 2, 1), (1, 2, 0), (0, 2, 0), (2, 1, 0), (1, 1, 0),
+                                  (0, 1, 0), (1, 0, 0)):
             eng.set_option("GEMM16_TAIL", tail)
             eng.set_option("GEMM16_PERSIST", persist)
+            eng.set_option("X16_KM", km)
             eng.encode_fbank(fb, fr)
             assert eng.device_flags() == 0
             outs.append([t.cpu() for t in eng.encoder_results()])
     finally:
         eng.set_option("GEMM16_TAIL", 2)
         eng.set_option("GEMM16_PERSIST", 2)
+        eng.set_option("X16_KM", 1)
     for got in outs[1:]:
         for a, b in zip(outs[0], got):
             assert torch.equal(a, b)

@@ -170,7 +170,8 @@ int main(int argc, char** argv) {
                                "pp:contig-no-mfma", "pp:dma-only", "pp:mfma+lds", "pp:lds-only", "w4",
                                "w4:no-dma", "w4:no-mfma", "w4:no-stores", "w4:mfma+lds", "pp:km"};
         const int nv = getenv("PP_ONLY") ? 0 : 15;
-        for (int rep = 0; rep < 3; ++rep)
+        const int nrep = getenv("PP_REPS") ? atoi(getenv("PP_REPS")) : 3;
+        for (int rep = 0; rep < nrep; ++rep)
           for (int v = nv ? 0 : 1; v < 16; v = (nv || v != 1) ? v + 1 : 15) {
             const int iters = 10;
             CK(hipEventRecord(e0));
