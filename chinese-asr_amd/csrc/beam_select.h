@@ -415,7 +415,66 @@ __device__ __forceinline__ void beam_select_block(const BeamSelArgs& a, int b, B
   // distinct slots; the (-inf, INT_MAX) sentinels that fill short lists land on slots only
   // sentinels reach.  Same list, in the same order, as the one-wave sorted-list merge (TopList +
   // wave_merge) this replaces.
-  {
+  // (round 5) K2 = 16 (k <= 8: at most 8 lists of 16): wave 0 merges them in registers instead, a
+  // bitonic network over 128 slots (2 per lane, lists of n2k padded with sentinels to 16): per level
+  // (32, 64, 128 slots) a flip step (slot s against its mirror in the block) and half-cleaners, each
+  // compare-exchange keeping the better (better()) in the lower slot.  better() is a total order on
+  // the real candidates (distinct indices) and the sentinels are identical, so the merged order, and
+  // with it the top 2k, is the tree's.  No block barrier after the row phase.
+  if constexpr (K2 == 16) {
+    if (wv == 0) {
+      float v0, v1;
+      int i0, i1;
+      auto ld = [&](int s, float& v, int& i) {
+        const int j = s >> 4, p = s & 15;
+        const bool ok = j < nrows && p < n2k;
+        v = ok ? S.rv[j][p] : -INFINITY;
+        i = ok ? S.ri[j][p] : 0x7fffffff;
+      };
+      ld(ln, v0, i0);
+      ld(64 + ln, v1, i1);
+      // compare-exchange of (v, i) with the same register of lane ln ^ mask; lo keeps the better
+      auto cx = [&](float& v, int& i, int mask, bool lo) {
+        const float pv = __shfl_xor(v, mask);
+        const int pi = __shfl_xor(i, mask);
+        if (lo == better(pv, pi, v, i)) {
+          v = pv;
+          i = pi;
+        }
+      };
+      auto cleaners = [&](int d0) {
+        for (int d = d0; d >= 1; d >>= 1) {
+          cx(v0, i0, d, (ln & d) == 0);
+          cx(v1, i1, d, (ln & d) == 0);
+        }
+      };
+      cx(v0, i0, 31, (ln & 16) == 0);  // 32-slot blocks (list pairs): flip, then cleaners
+      cx(v1, i1, 31, (ln & 16) == 0);
+      cleaners(8);
+      cx(v0, i0, 63, (ln & 32) == 0);  // 64-slot blocks (one register each)
+      cx(v1, i1, 63, (ln & 32) == 0);
+      cleaners(16);
+      {  // 128 slots: slot s of register 0 against slot 127 - s (register 1 of lane 63 - ln)
+        const float p0v = __shfl_xor(v1, 63), p1v = __shfl_xor(v0, 63);
+        const int p0i = __shfl_xor(i1, 63), p1i = __shfl_xor(i0, 63);
+        if (better(p0v, p0i, v0, i0)) {
+          v0 = p0v;
+          i0 = p0i;
+        }
+        if (!better(p1v, p1i, v1, i1)) {
+          v1 = p1v;
+          i1 = p1i;
+        }
+      }
+      cleaners(32);
+      if (ln < n2k) {
+        S.cv[ln] = v0;
+        S.ci[ln] = i0;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
+  } else {
     float(*sv)[K2] = S.rv;
     int(*si)[K2] = S.ri;
     float(*dv)[K2] = S.rv2;
@@ -457,8 +516,8 @@ __device__ __forceinline__ void beam_select_block(const BeamSelArgs& a, int b, B
       S.cv[tid] = sv[0][tid];
       S.ci[tid] = si[0][tid];
     }
+    __syncthreads();
   }
-  __syncthreads();
   stamp(5, (uint32_t)__builtin_amdgcn_s_memrealtime());
 
   // bookkeeping, one lane of wave 0 per ranked candidate c < 2k (the serial loops of

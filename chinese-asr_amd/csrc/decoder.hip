@@ -60,6 +60,12 @@ constexpr int DG_BK = 64;
 #ifndef CASR_DG_DIAG
 #define CASR_DG_DIAG 0
 #endif
+// (round 5) the projection epilogue's row partials take exp(x - max) as v_exp_f32 of (x - max)
+// log2(e) instead of the libm expf (about 15 instructions each, 7 x 16 per lane and block in the beam
+// shape); 0 restores expf (diagnostic builds, tools/probes/ab_libs.sh)
+#ifndef CASR_FAST_PART_EXP
+#define CASR_FAST_PART_EXP 1
+#endif
 
 __device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
   const int L = blockIdx.x, x = L & 7, j = L >> 3;
@@ -781,7 +787,9 @@ __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const f
 
 // per-row partials over the block's columns n < V (greedy, and beam at temperature 1): lane (g, u)
 // holds columns 16 (nb NTN + tn) + u; the 16 lanes of one g share the rows
-template <int NTN>
+// IX: also the first column of the maximum (the greedy select's token; the beam select reads only
+// the maximum and the sum)
+template <int NTN, bool IX = true>
 __device__ __forceinline__ void proj_row_partials(const f32x4 (&acc)[NTN], const float (&bn)[16], int row0, int nb,
                                                   int u, const GreedyPart& gp, int R, int V) {
 #pragma unroll
@@ -793,28 +801,37 @@ __device__ __forceinline__ void proj_row_partials(const f32x4 (&acc)[NTN], const
     for (int tn = 0; tn < NTN; ++tn) {
       const int n = (nb * NTN + tn) * 16 + u;
       x[tn] = acc[tn][e] + bn[tn];
-      if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
-        m = x[tn];
-        mi = n;
+      if constexpr (IX) {
+        if (n < V && x[tn] > m) {  // columns ascend with tn: first index within the lane
+          m = x[tn];
+          mi = n;
+        }
+      } else if (n < V) {
+        m = fmaxf(m, x[tn]);
       }
     }
     {  // the row's (max, lowest column among equal maxima) over the 16 lanes of this g
       const float rm = row16_max(m);
-      mi = row16_min(m == rm ? mi : 0x7fffffff);
+      if constexpr (IX) mi = row16_min(m == rm ? mi : 0x7fffffff);
       m = rm;
     }
+    // sum of exp(x - max): v_exp_f32 (1 ulp) of (x - max) log2(e), whose product rounding adds at most
+    // |x - max| 2^-24 relative to a term (<= 1e-6 for the terms above 4e-8), so the row's logsumexp
+    // moves by ~1e-6: the select's values x - lse + score move together per row, and the scores stay
+    // far inside their 2e-3 tolerance (the GPU suite passes unchanged; A/B: fused GEMM 3.9 -> 3.8 ms
+    // per beam batch, profiles/r05/fastexp/)
     float sx = 0.f;
 #pragma unroll
     for (int tn = 0; tn < NTN; ++tn) {
       const int n = (nb * NTN + tn) * 16 + u;
-      if (n < V) sx += expf(x[tn] - m);
+      if (n < V) sx += CASR_FAST_PART_EXP ? __builtin_amdgcn_exp2f((x[tn] - m) * 1.4426950408889634f) : expf(x[tn] - m);
     }
     sx = row16_sum(sx);  // lane u == 0 (the row's first quad) writes it
     const int row = row0 + e;
     if (u == 0 && row < R) {
       gp.mx[(size_t)row * GP_NB + nb] = m;
       gp.se[(size_t)row * GP_NB + nb] = sx;
-      gp.ix[(size_t)row * GP_NB + nb] = mi;
+      if constexpr (IX) gp.ix[(size_t)row * GP_NB + nb] = mi;
     }
   }
 }
@@ -852,7 +869,10 @@ struct ProjEpi {
                                       float* scr) const {
     static_assert(NTN <= 16, "bias prefetch slots");
     if (logits) proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, GP_NT);
-    if (gp.mx) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
+    if (gp.mx) {
+      if (logits) proj_row_partials<NTN, false>(acc, p.bn, row0, nb, u, gp, R, V);  // beam
+      else proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
+    }
   }
 };
 
@@ -900,7 +920,10 @@ struct FoldEpi {
       proj_logits_out<NTN>(acc, p.bn, row0, nb, u, scr, logits, gp.tmx, R, V, VT, has_gates ? gates : nullptr,
                            16 * VG);
     if (nb * NTN >= VT) return;  // no vocabulary tile in this block
-    if (gp.mx) proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
+    if (gp.mx) {
+      if (logits) proj_row_partials<NTN, false>(acc, p.bn, row0, nb, u, gp, R, V);  // beam
+      else proj_row_partials<NTN>(acc, p.bn, row0, nb, u, gp, R, V);
+    }
   }
 };
 
