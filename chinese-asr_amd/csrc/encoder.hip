@@ -430,6 +430,10 @@ constexpr int KR_G = 16;                   // A rows per item
 constexpr int KR_KT = C / 32;              // 32-deep k-tiles
 constexpr int KR_IF = KR_KT * KR_G * 32;   // floats per item (32 KB)
 constexpr int KR_NBUF = 4;                 // ring slots (three items in flight)
+// 16-k-major items (km): a row's 64-B piece of a block in LDS, sub-chunk s at slot s ^ kr_swz(row):
+// the swizzle {0, 2, 3, 1} by row / 4 keeps every ds_read_b128 lane group of the (row r, chunk g)
+// fragment reads on 16 distinct bank groups, for the hi (s = g & 1) and the lo (s = 2 + (g & 1)) reads
+CASR_DEV int kr_swz(int row) { return (120 >> (2 * ((row >> 2) & 3))) & 3; }
 
 __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict__ enc16, const float* __restrict__ w16,
                                                         const float* __restrict__ bias, float* __restrict__ keysT,
@@ -464,13 +468,18 @@ __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict_
     float* dst = ring + (q % KR_NBUF) * KR_IF;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int i = w + 8 * u, kt = i >> 1, h = i & 1;
-      const int row = 8 * h + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
-      const int t = min(KR_G * j + row, Tp - 1);
-      const size_t gr = (size_t)b * Tp + t;
-      const float* src = km ? enc16 + ((size_t)(2 * kt + ((c >> 1) & 1)) * Mimg + gr) * 16 + 4 * ((c & 1) + 2 * (c >> 2))
-                            : enc16 + gr * C + kt * 32 + 4 * c;
-      if (!(CASR_KR_DIAG & 1)) lds_dma16(src, dst + (kt * KR_G + 8 * h) * 32);
+      const int i = w + 8 * u;
+      if (km) {  // instruction i: 16-k block i of the 16 rows, 1 KB contiguous; slot s of a row holds
+                 // sub-chunk s ^ kr_swz(row)
+        const int row = lane >> 2, c = (lane & 3) ^ kr_swz(row);
+        const size_t gr = (size_t)b * Tp + min(KR_G * j + row, Tp - 1);
+        if (!(CASR_KR_DIAG & 1)) lds_dma16(enc16 + ((size_t)i * Mimg + gr) * 16 + 4 * c, dst + i * KR_G * 16);
+      } else {
+        const int kt = i >> 1, h = i & 1;
+        const int row = 8 * h + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+        const size_t gr = (size_t)b * Tp + min(KR_G * j + row, Tp - 1);
+        if (!(CASR_KR_DIAG & 1)) lds_dma16(enc16 + gr * C + kt * 32 + 4 * c, dst + (kt * KR_G + 8 * h) * 32);
+      }
     }
   };
   // VMEM operations this wave issued after the DMA of item q, at the top of iteration q: each
@@ -507,12 +516,19 @@ __global__ __launch_bounds__(512, 1) void keys16_kernel(const float* __restrict_
     if (q + KR_NBUF - 1 < nitems) stage(q + KR_NBUF - 1);
     const float* as = ring + (q % KR_NBUF) * KR_IF;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accx = {0.f, 0.f, 0.f, 0.f};
-    const int sw = (r >> 1) & 7;
+    const int sw = (r >> 1) & 7, swk = kr_swz(r);
 #pragma unroll
     for (int kt = 0; kt < KR_KT; ++kt) {
-      const float* ar = as + (kt * KR_G + r) * 32;
-      const f16x8 ah = *reinterpret_cast<const f16x8*>(ar + ((g ^ sw) << 2));
-      const f16x8 al = *reinterpret_cast<const f16x8*>(ar + (((4 + g) ^ sw) << 2));
+      f16x8 ah, al;
+      if (km) {  // hi chunk g of the 32-k tile = sub-chunk g & 1 of block 2 kt + (g >> 1); lo = 2 + (g & 1)
+        const float* ar = as + ((2 * kt + (g >> 1)) * KR_G + r) * 16;
+        ah = *reinterpret_cast<const f16x8*>(ar + (((g & 1) ^ swk) << 2));
+        al = *reinterpret_cast<const f16x8*>(ar + (((2 + (g & 1)) ^ swk) << 2));
+      } else {
+        const float* ar = as + (kt * KR_G + r) * 32;
+        ah = *reinterpret_cast<const f16x8*>(ar + ((g ^ sw) << 2));
+        al = *reinterpret_cast<const f16x8*>(ar + (((4 + g) ^ sw) << 2));
+      }
       if (!(CASR_KR_DIAG & 2)) mfma_s16(ah, al, wh[kt], wl[kt], acc, accx);
       else acc[0] += (float)ah[0] + (float)al[1];
     }

@@ -271,6 +271,9 @@ __global__ __launch_bounds__(RTH) void features_rows_kernel(const float* __restr
                                                             uint32_t* __restrict__ x16, int Kp,
                                                             int32_t* __restrict__ err, int km) {
   __shared__ __attribute__((aligned(16))) float xs[RNF * F];  // frames 3 j0 - 4 .. 3 (j0 + RJ) + 3
+  // km: per-wave transpose of a row pair, so a lane stores 16 B and 8 lanes one whole 128-B line (two
+  // adjacent rows' 64-B pieces of a 16-k block); 40-word pieces put the 8 blocks on distinct banks
+  __shared__ __attribute__((aligned(16))) uint32_t kx[X16 ? (RTH / 64) * 8 * 40 : 1];
   const int b = blockIdx.y, j0 = blockIdx.x * RJ, p = threadIdx.x;
   const int nf = min(max(frames[b], 0), T), lp = nf / 3;
   const int t_lo = 3 * j0 - 4;
@@ -306,6 +309,7 @@ __global__ __launch_bounds__(RTH) void features_rows_kernel(const float* __restr
 #pragma unroll
   for (int k = 0; k < 9; ++k) win[k] = *reinterpret_cast<const float2*>(xs + (r + k) * F + m);
   bool range_ok = true;
+  uint32_t ph = 0, pl = 0;  // km: the even row's hi / lo words, stored with the odd row
   const int jn = min(RJ, Tp - j0);
   for (int jj = 0; jj < jn; ++jj) {
     const int j = j0 + jj;
@@ -328,10 +332,31 @@ __global__ __launch_bounds__(RTH) void features_rows_kernel(const float* __restr
     if constexpr (X16) {
       const uint32_t w0 = split16_word(v.x), w1 = split16_word(v.y);
       // row image: 32-k tiles [32 hi | 32 lo] halves; km: 16-k-block major [Kp / 16][B Tp][16 hi | 16 lo]
-      uint32_t* row = km ? x16 + ((size_t)(o0 >> 4) * gridDim.y * Tp + (size_t)b * Tp + j) * 16 + ((o0 & 15) >> 1)
-                         : x16 + ((size_t)b * Tp + j) * Kp + (o0 >> 5) * 32 + ((o0 & 31) >> 1);
-      row[0] = (w0 & 0xFFFFu) | (w1 << 16);               // hi halves of columns o0, o0 + 1
-      row[km ? 8 : 16] = (w0 >> 16) | (w1 & 0xFFFF0000u);  // lo halves
+      const uint32_t hw = (w0 & 0xFFFFu) | (w1 << 16), lw = (w0 >> 16) | (w1 & 0xFFFF0000u);  // hi / lo halves
+      if (km && (jj & 1)) {  // rows j - 1, j (j0 is even): one 128-B line per 16-k block
+        uint32_t* sc = kx + (p >> 6) * 320 + ((p & 63) >> 3) * 40;
+        const int wl = p & 7;
+        sc[wl] = ph;
+        sc[8 + wl] = pl;
+        sc[16 + wl] = hw;
+        sc[24 + wl] = lw;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint4 q = *reinterpret_cast<const uint4*>(sc + 4 * wl);
+        *reinterpret_cast<uint4*>(x16 + ((size_t)(o0 >> 4) * gridDim.y * Tp + (size_t)b * Tp + j - 1) * 16 + 4 * wl) = q;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else if (km && jj + 1 < jn) {
+        ph = hw;
+        pl = lw;
+      } else {
+        uint32_t* row = km ? x16 + ((size_t)(o0 >> 4) * gridDim.y * Tp + (size_t)b * Tp + j) * 16 + ((o0 & 15) >> 1)
+                           : x16 + ((size_t)b * Tp + j) * Kp + (o0 >> 5) * 32 + ((o0 & 31) >> 1);
+        row[0] = hw;
+        row[km ? 8 : 16] = lw;
+      }
       const float ax = fabsf(v.x), ay = fabsf(v.y);
       range_ok &= !(ax >= 65520.f && ax < INFINITY) && !(ay >= 65520.f && ay < INFINITY);
     } else {

@@ -639,12 +639,14 @@ __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restri
 // counted vmcnt waits and a raw s_barrier per stage.  The MFMAs per accumulator are compute() of
 // gemm16_bias_kernel (same fragments, order and 2^11 scaling), and the epilogue its slab form: the
 // same bits.
-// km: A (rows r0 .. r0 + M - 1 of an Mimg-row image) and W 16-k-block major; else row images (A16 at
-// row r0 already)
-template <int RT>
+// KM: A (rows r0 .. r0 + M - 1 of an Mimg-row image) and W 16-k-block major, and a stage in LDS is
+// [16-k block 0 | block 1] x [A rows | W rows] x 64 B (the ping-pong kernel's rows: chunk c of a row at
+// c ^ ((row >> 2) & 3)), so each DMA instruction reads 16 rows of one block, 1 KB contiguous; else
+// row images (A16 at row r0 already) and [rows] x 128 B stages
+template <int RT, bool KM>
 __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
                                                              const float* __restrict__ bias, float* __restrict__ Cout,
-                                                             int M, int N, int Kp, int km, int r0, int Mimg) {
+                                                             int M, int N, int Kp, int r0, int Mimg) {
   constexpr int BM = 32 * RT, BN = 128, ROWS = BM + BN, STF = ROWS * G16_K;  // floats per stage
   constexpr int NBUF = 4, NI = ROWS / 8, PW = (NI + 3) / 4;  // DMA instructions per stage / per wave
   static_assert(NBUF * STF * 4 <= 160 * 1024 && (NBUF - 2) * PW < 64, "ring fits the LDS; vmcnt range");
@@ -658,6 +660,24 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
   for (int i = 0; i < RT; ++i)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+  // KM: instruction j's source walks two 16-k blocks per stage; its pointer is advanced after each
+  // stage is issued (stages are issued in order), so a stage costs no address arithmetic
+  const float* ksrc[PW];
+  size_t kinc[PW];
+  int kdst[PW];
+  if constexpr (KM) {
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const int i = min(wave + 4 * j, NI - 1);
+      const int h = i / (NI / 2), q = i - h * (NI / 2), row = 16 * q + (lane >> 2);
+      const int c = (lane & 3) ^ ((row >> 2) & 3);
+      const bool isa = 16 * q < BM;
+      ksrc[j] = isa ? A16 + ((size_t)h * Mimg + r0 + min(m0 + row, M - 1)) * 16 + 4 * c
+                    : W16 + ((size_t)h * N + n0 + row - BM) * 16 + 4 * c;
+      kinc[j] = (size_t)2 * (isa ? Mimg : N) * 16;
+      kdst[j] = (h * ROWS + 16 * q) * 16;
+    }
+  }
   auto stage = [&](int kt) {
     float* dst = ring + (kt % NBUF) * STF;
     const int k0 = kt * G16_K;
@@ -665,16 +685,15 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
     for (int j = 0; j < PW; ++j) {
       const int i = wave + 4 * j;
       if (i < NI) {
-        const int row = 8 * i + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
-        const int ar = min(m0 + row, M - 1), wr = n0 + row - BM;
-        const float* src;
-        if (km) {  // chunk c of the 32-k tile: sub-chunk (c & 1) + 2 (c >> 2) of 16-k block 2 kt + ((c >> 1) & 1)
-          const size_t blk = (size_t)(2 * kt + ((c >> 1) & 1)), sub = 4 * ((c & 1) + 2 * (c >> 2));
-          src = row < BM ? A16 + (blk * Mimg + r0 + ar) * 16 + sub : W16 + (blk * N + wr) * 16 + sub;
+        if constexpr (KM) {  // instruction i: 16-k block h, 16 rows (A, then W) of it
+          lds_dma16(ksrc[j], dst + kdst[j]);
+          ksrc[j] += kinc[j];
         } else {
-          src = row < BM ? A16 + (size_t)ar * Kp + k0 + 4 * c : W16 + (size_t)wr * Kp + k0 + 4 * c;
+          const int row = 8 * i + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+          const int ar = min(m0 + row, M - 1), wr = n0 + row - BM;
+          lds_dma16(row < BM ? A16 + (size_t)ar * Kp + k0 + 4 * c : W16 + (size_t)wr * Kp + k0 + 4 * c,
+                    dst + 8 * i * G16_K);
         }
-        lds_dma16(src, dst + 8 * i * G16_K);
       }
     }
   };
@@ -683,15 +702,22 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int ch = 2 * ks + hsel;  // 16-B chunk of this lane's 8 k (hi); lo is chunk 4 + ch
-      const int wrow = BM + wave * 32 + r32, wsw = (wrow >> 1) & 7;
-      const f16x8 wh = *reinterpret_cast<const f16x8*>(src + wrow * G16_K + ((ch ^ wsw) << 2));
-      const f16x8 wl = *reinterpret_cast<const f16x8*>(src + wrow * G16_K + (((4 + ch) ^ wsw) << 2));
+      // KM: block ks holds [hi 0-7 | hi 8-15 | lo 0-7 | lo 8-15] of each row: chunks hsel and 2 + hsel
+      auto frag = [&](int row, bool lo) -> f16x8 {
+        if constexpr (KM)
+          return *reinterpret_cast<const f16x8*>(src + (ks * ROWS + row) * 16 + ((((lo ? 2 : 0) + hsel) ^ ((row >> 2) & 3)) << 2));
+        else
+          return *reinterpret_cast<const f16x8*>(src + row * G16_K + ((((lo ? 4 : 0) + ch) ^ ((row >> 1) & 7)) << 2));
+      };
+      const int wrow = BM + wave * 32 + r32;
+      const f16x8 wh = frag(wrow, false);
+      const f16x8 wl = frag(wrow, true);
       const f16x8 w1 = wh * two11;
 #pragma unroll
       for (int tm = 0; tm < RT; ++tm) {
-        const int row = tm * 32 + r32, sw = (row >> 1) & 7;
-        const f16x8 ah = *reinterpret_cast<const f16x8*>(src + row * G16_K + ((ch ^ sw) << 2));
-        const f16x8 al = *reinterpret_cast<const f16x8*>(src + row * G16_K + (((4 + ch) ^ sw) << 2));
+        const int row = tm * 32 + r32;
+        const f16x8 ah = frag(row, false);
+        const f16x8 al = frag(row, true);
         acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w1, acc[tm], 0, 0, 0);
         acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl, acc[tm], 0, 0, 0);
         acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh, acc[tm], 0, 0, 0);
@@ -745,11 +771,11 @@ static bool launch_tail_balanced(const float* A16, const float* W16, const float
   const int RT = std::min(5, (units + ncu - 1) / ncu);  // (past 5 x ncu units: more than one round)
   const int blocks = (Mt + 32 * RT - 1) / (32 * RT) * (N / 128);
   switch (RT) {
-    case 1: hipLaunchKernelGGL(gemm16_tail_kernel<1>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
-    case 2: hipLaunchKernelGGL(gemm16_tail_kernel<2>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
-    case 3: hipLaunchKernelGGL(gemm16_tail_kernel<3>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
-    case 4: hipLaunchKernelGGL(gemm16_tail_kernel<4>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
-    default: hipLaunchKernelGGL(gemm16_tail_kernel<5>, dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, km, r0, Mimg); break;
+    case 1: hipLaunchKernelGGL((km ? gemm16_tail_kernel<1, true> : gemm16_tail_kernel<1, false>), dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, r0, Mimg); break;
+    case 2: hipLaunchKernelGGL((km ? gemm16_tail_kernel<2, true> : gemm16_tail_kernel<2, false>), dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, r0, Mimg); break;
+    case 3: hipLaunchKernelGGL((km ? gemm16_tail_kernel<3, true> : gemm16_tail_kernel<3, false>), dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, r0, Mimg); break;
+    case 4: hipLaunchKernelGGL((km ? gemm16_tail_kernel<4, true> : gemm16_tail_kernel<4, false>), dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, r0, Mimg); break;
+    default: hipLaunchKernelGGL((km ? gemm16_tail_kernel<5, true> : gemm16_tail_kernel<5, false>), dim3(blocks), dim3(256), 0, s, A16, W16, bias, Gin, Mt, N, Kp, r0, Mimg); break;
   }
   return true;
 }

@@ -201,6 +201,34 @@ int main(int argc, char** argv) {
             printf("Kp %d %-14s %8.1f us  %6.0f TF/s f16 (K used %d)\n", Kp, names[v], 1000.0 * ms / iters,
                    flop / (ms / iters * 1e-3) / 1e12, 16 * nk16);
           }
+        // balanced tail form over the last 2560 rows (RT 5, 256 workgroups): row image vs 16-k-major
+        const int Mt = 2560, r0 = M - Mt, tb = Mt / 160 * (N / 128);
+        auto run_tail = [&](bool km, float* C) {
+          if (km)
+            hipLaunchKernelGGL((gemm16_tail_kernel<5, true>), dim3(tb), dim3(256), 0, 0, dAk, dWk, dB, C, Mt, N, Kp, r0, M);
+          else
+            hipLaunchKernelGGL((gemm16_tail_kernel<5, false>), dim3(tb), dim3(256), 0, 0, dA + (size_t)r0 * Kp, dW, dB, C,
+                               Mt, N, Kp, r0, M);
+        };
+        run_tail(false, dC0);
+        run_tail(true, dC1);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(c0.data(), dC0, (size_t)Mt * N * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(c1.data(), dC1, (size_t)Mt * N * 4, hipMemcpyDeviceToHost));
+        size_t tdiff = 0;
+        for (size_t i = 0; i < (size_t)Mt * N; ++i) tdiff += memcmp(&c0[i], &c1[i], 4) != 0;
+        printf("Kp %d tail rows %d: row image vs km: %zu differing\n", Kp, Mt, tdiff);
+        for (int rep = 0; rep < 3; ++rep)
+          for (int km = 0; km < 2; ++km) {
+            const int iters = 20;
+            CK(hipEventRecord(e0));
+            for (int i = 0; i < iters; ++i) run_tail(km, dC1);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            printf("Kp %d tail%-10s %8.1f us\n", Kp, km ? ":km" : "", 1000.0 * ms / iters);
+          }
       }
       CK(hipFree(dA));
       CK(hipFree(dW));
