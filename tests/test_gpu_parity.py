@@ -807,6 +807,31 @@ def test_input_gemm_tail_split_bitwise(eng, B):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("T", [809, 803, 47, 50])
+def test_features_km_row_pairs_any_tail(eng, T):
+    """The feature kernel's 16-k-major image stores go out a row pair at a time (a wave-private
+    transpose into whole 128-B lines); a block whose last row has no partner (T' = T // 3 with an
+    odd number of rows in the last 16-row block: T' = 269, 267, 15) stores that row alone.  The
+    encoder outputs through casr_encode_fbank with the 16-k-major images equal those with row
+    images bit for bit, ragged lengths included."""
+    if eng.precision() != "s16x3":
+        pytest.skip("the split-f16 images only")
+    bind(eng, "peaked")
+    frames = [T, T - 4, max(3, T // 2), 7]
+    fb, fr = batch_fbank(frames, eng.device)
+    outs = []
+    try:
+        for km in (1, 0):
+            eng.set_option("X16_KM", km)
+            eng.encode_fbank(fb, fr)
+            assert eng.device_flags() == 0
+            outs.append([t.cpu() for t in eng.encoder_results()])
+    finally:
+        eng.set_option("X16_KM", 1)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B", [1, 33, 129])
 def test_odd_batches_greedy_match_oracle(eng, B):
     """Batch sizes at the layout boundaries, through casr_encode_fbank (T = 60, T' = 20, ragged
