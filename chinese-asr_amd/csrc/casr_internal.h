@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1, 1};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -381,6 +381,11 @@ struct FoldBufs {
 hipError_t build_fold(const float* W, const Layout& L, int V, float* wfold, float* emb_gates, float* wq16,
                       float* wfold32, hipStream_t s);
 
+// the greedy folded GEMM's k split at R <= 32 (decoder.hip dgemm_kernel KS): DG_KS blocks per
+// output block, at most DG_KS_GROUPS output blocks of 2 epilogue waves
+constexpr int DG_KS = 4, DG_KS_GROUPS = 64, DG_KS_COUNTERS = 2 * DG_KS_GROUPS;
+constexpr size_t DG_KS_PART_BYTES = (size_t)DG_KS_COUNTERS * DG_KS * FOLD_NT * 64 * 16;  // f32x4 per lane
+
 struct DecodeBufs {
   float* st[2];          // [R][ST]
   float* logits;         // [R][V]
@@ -400,6 +405,9 @@ struct DecodeBufs {
   float* rec_score;      // [B][L][k]
   int32_t* rec_src;      // [B][L][k]
   uint8_t* rec_valid;    // [B][L][k]
+  // greedy at R <= 32 with CASR_OPT_DEC_KSPLIT: the k-range sums and arrival counters (else nullptr)
+  float* kspart;         // [groups][2 waves][DG_KS][FOLD_NT tiles][64 lanes] x 4 floats
+  int32_t* kscnt;
 };
 
 struct DecodeArgs {

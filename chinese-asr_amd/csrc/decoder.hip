@@ -57,6 +57,7 @@ namespace casr {
 // NR row blocks of one weight column slice get ids with the same L % 8: the slice is fetched into
 // one XCD's L2 once and re-read from there by every row block.
 constexpr int DG_BK = 64;
+typedef float ks_f2 __attribute__((ext_vector_type(2)));  // (the k split's 8-byte exchange words)
 #ifndef CASR_DG_DIAG
 #define CASR_DG_DIAG 0
 #endif
@@ -67,8 +68,9 @@ constexpr int DG_BK = 64;
 #define CASR_FAST_PART_EXP 1
 #endif
 
-__device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb) {
-  const int L = blockIdx.x, x = L & 7, j = L >> 3;
+__device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb, int L = -1) {
+  if (L < 0) L = blockIdx.x;
+  const int x = L & 7, j = L >> 3;
   nb = (j / NR) * 8 + x;
   rb = j % NR;
   return nb < NB;
@@ -132,10 +134,17 @@ __device__ __forceinline__ void static_for(F&& f) {
 // counted wait for stage kt retires only W(kt) (and what preceded it) while A(kt + SA - 2) stays in
 // flight: the chain waits on a 28 KB W stage instead of a 60 KB [A | W] one.  Same operands, same
 // order per element: bitwise equal to SA = S.
+// KS > 1 (the greedy folded GEMM at R <= 32, CASR_OPT_DEC_KSPLIT: its 63 blocks of 32 x 112 would
+// leave three quarters of the CUs idle): KS blocks per output block, block q of them multiplies the
+// 64-deep tiles q nkt / KS .. (q + 1) nkt / KS - 1 (the in-block k slices as usual).  Each epilogue
+// wave stores its k-range sum to kspart, and the wave that arrives last at its counter (kscnt,
+// agent-scope fences around an atomic add) adds the KS sums in q order, resets the counter and runs
+// the epilogue: a fixed order, so the bits do not depend on which block arrives last.
 template <int WR, int NT, int S, class ASrc, class Epi, bool S16 = false, int RS = 1, int WC = 1, bool IL = false,
-          int BKW = 64, bool ONE = false, int SA = S>
+          int BKW = 64, bool ONE = false, int SA = S, int KS = 1>
 __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntiles, int nkt,
-                                                    const float* __restrict__ Wf, ASrc asrc, Epi epi) {
+                                                    const float* __restrict__ Wf, ASrc asrc, Epi epi,
+                                                    f32x4* __restrict__ kspart, int* __restrict__ kscnt) {
   constexpr int KQ = 8 / (WR * WC), QPW = 4 / KQ, BM = 16 * WR * RS, NTW = NT / WC;
   static_assert(WR * WC * KQ == 8 && NT % WC == 0 && KQ <= 4, "8 waves = row groups x column groups x k slices");
   constexpr bool B32 = BKW == 32;
@@ -154,6 +163,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   constexpr bool ASYM = SA > S;
   constexpr int JA = NA / 8;  // ASYM: slots j < JA are A DMAs in every wave, the rest W
   static_assert(!ASYM || (S == 2 && SA <= 4 && NA % 8 == 0 && JA < NSLOT), "deeper A ring: S = 2, whole A slots");
+  static_assert(KS == 1 || (!ASYM && !B32 && KQ > 1), "k split: the 64-deep ring, k slices exchanged in LDS");
   __shared__ __attribute__((aligned(16))) float lb0[STG];
   __shared__ __attribute__((aligned(16))) float lb1[STG];
   __shared__ __attribute__((aligned(16))) float lb2[S > 2 ? STG : 4];
@@ -178,7 +188,9 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
     else return lb5;
   };
   int nb, rb;
-  if (!xcd_tile(NB, NR, nb, rb)) return;
+  const int ksq = KS > 1 ? (int)(blockIdx.x % KS) : 0;  // this block's k range of the output block
+  if (!xcd_tile(NB, NR, nb, rb, KS > 1 ? (int)(blockIdx.x / KS) : -1)) return;
+  const int nktl = nkt / KS, kofs = ksq * nktl;  // 64-deep tiles of this block, the first one
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ws = w % WR, wc = (w / WR) % WC, kq = w / (WR * WC);
   uint32_t* dtr = g_dg_trace ? g_dg_trace + ((size_t)Epi::kTraceClass * 4096 + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int i) {
@@ -241,7 +253,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
   auto stage_slot2 = [&](float* la, float* lw, int kt, auto J) {
     constexpr int j = decltype(J)::value;
     if constexpr (j < NSLOT) {
-      const int kb = B32 ? kt >> 1 : kt, k0 = kb * 64;
+      const int kb = (B32 ? kt >> 1 : kt) + kofs, k0 = kb * 64;
       const int i = w + 8 * j;
       if (i < NA) {
         const float* seg;
@@ -363,7 +375,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
     });
   } else {
     static_for<0, S - 1>([&](auto I) {
-      if (I < nkt) stage(buf(I), I);
+      if (I < nktl) stage(buf(I), I);
     });
   }
   // after the first ring stages are in flight: the epilogue's operands (bias, predecessor rows,
@@ -414,19 +426,19 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
       });
     }
   }
-  for (int kt0 = 0; !ASYM && kt0 < nkt; kt0 += S) {
+  for (int kt0 = 0; !ASYM && kt0 < nktl; kt0 += S) {
     static_for<0, S>([&](auto I) {
       const int kt = kt0 + I;
-      if (kt >= nkt) return;
+      if (kt >= nktl) return;
       // this wave's DMA of tile kt is done once at most (tiles issued after it) x cnt_w remain
-      const int ahead = min(S - 2, nkt - 1 - kt);
+      const int ahead = min(S - 2, nktl - 1 - kt);
       vm_wait_le<(S - 2) * NSLOT>(ahead * cnt_w);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of tile kt-1 are done
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");  // no LDS read of tile kt moves above the barrier
       // CASR_DG_DIAG (diagnostic builds, tools/probes): bit 0 drops the k loop's DMA, bit 1 the MFMAs
       auto issue = [&](auto J) {
-        if (kt + S - 1 < nkt && !(CASR_DG_DIAG & 1))
+        if (kt + S - 1 < nktl && !(CASR_DG_DIAG & 1))
           stage_slot(buf(std::integral_constant<int, (I + S - 1) % S>{}), kt + S - 1, J);
       };
       if constexpr (!ILS) static_for<0, NSLOT>(issue);
@@ -478,6 +490,45 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
 #pragma unroll
         for (int tn = 0; tn < NTW; ++tn) acc[rs][tn] += part(j, rs, tn);
   }
+  if constexpr (KS > 1) {  // the KS k ranges of this wave's rows and columns, summed in q order
+    // agent-scope (sc1) 8-byte stores and loads, as the recurrence's hand-off words: coherent across
+    // the XCDs' L2s without the L2 write-back / invalidate a device-scope fence costs (measured: the
+    // fenced form took 33 us per step against 19.5 for the unsplit GEMM)
+    const size_t gi = ((size_t)rb * NB + nb) * (WR * WC) + ws * WC + wc;
+    uint64_t* pk = reinterpret_cast<uint64_t*>(kspart + gi * (KS * RS * NTW * 64)) + 2 * lane;
+    auto slot = [&](int qq, int rs, int tn) { return pk + (size_t)((qq * RS + rs) * NTW + tn) * 128; };
+#pragma unroll
+    for (int rs = 0; rs < RS; ++rs)
+#pragma unroll
+      for (int tn = 0; tn < NTW; ++tn) {
+        const f32x4 v = acc[rs][tn];
+        uint64_t* p = slot(ksq, rs, tn);
+        __hip_atomic_store(p, __builtin_bit_cast(uint64_t, (ks_f2){v[0], v[1]}), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p + 1, __builtin_bit_cast(uint64_t, (ks_f2){v[2], v[3]}), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    vm_wait<0>();  // the sums are stored before the count
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(kscnt + gi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0);
+    if (old != KS - 1) return;
+#pragma unroll
+    for (int rs = 0; rs < RS; ++rs)
+#pragma unroll
+      for (int tn = 0; tn < NTW; ++tn) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int qq = 0; qq < KS; ++qq) {
+          const uint64_t* p = slot(qq, rs, tn);
+          const ks_f2 lo = __builtin_bit_cast(ks_f2, __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          const ks_f2 hi = __builtin_bit_cast(ks_f2, __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          const f32x4 w = {lo[0], lo[1], hi[0], hi[1]};
+          v = qq == 0 ? w : v + w;
+        }
+        acc[rs][tn] = v;
+      }
+    if (lane == 0) __hip_atomic_store(kscnt + gi, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  }
   // lane holds rows erow0(rs) + e (e = 0..3), column (nbw*NTW + tn)*16 + r
   // per-wave LDS scratch for the epilogue (ring buffers are free now; the k-slice exchange
   // above used lb0 (only when KQ > 1, i.e. at most 4 epilogue waves, all on lb1)): 16 rows x
@@ -491,21 +542,30 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
 }
 
 template <int WR, int NT, int S, int RS = 1, int WC = 1, bool IL = false, int BKW = 64, bool ONE = false, int SA = S,
-          class ASrc, class Epi>
+          int KS = 1, class ASrc, class Epi>
 static void launch_dg(int NB, int R, int ntiles, int nkt, const float* Wf, const ASrc& asrc, const Epi& epi,
-                      int s16, hipStream_t s) {
+                      int s16, hipStream_t s, f32x4* kspart = nullptr, int* kscnt = nullptr) {
   constexpr int BM = 16 * WR * RS;
   const int NR = (R + BM - 1) / BM;
+  if constexpr (KS > 1) {  // (64-deep stages, nkt % KS == 0: the host's check)
+    if (s16)
+      hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL, 64, false, S, KS>),
+                         dim3(xcd_grid(NB, NR) * KS), dim3(512), 0, s, NB, NR, ntiles, nkt, Wf, asrc, epi, kspart, kscnt);
+    else
+      hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, false, RS, WC, false, 64, false, S, KS>),
+                         dim3(xcd_grid(NB, NR) * KS), dim3(512), 0, s, NB, NR, ntiles, nkt, Wf, asrc, epi, kspart, kscnt);
+    return;
+  }
   if constexpr (BKW == 32 || ONE) {  // s16 only (the f32 form of the same shape does not fit the LDS)
     hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL, BKW, ONE, SA>), dim3(xcd_grid(NB, NR)),
-                       dim3(512), 0, s, NB, NR, ntiles, nkt * (64 / BKW), Wf, asrc, epi);
+                       dim3(512), 0, s, NB, NR, ntiles, nkt * (64 / BKW), Wf, asrc, epi, nullptr, nullptr);
   } else {
     if (s16)
       hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, true, RS, WC, IL>), dim3(xcd_grid(NB, NR)), dim3(512), 0,
-                         s, NB, NR, ntiles, nkt, Wf, asrc, epi);
+                         s, NB, NR, ntiles, nkt, Wf, asrc, epi, nullptr, nullptr);
     else
       hipLaunchKernelGGL((dgemm_kernel<WR, NT, S, ASrc, Epi, false, RS, WC>), dim3(xcd_grid(NB, NR)), dim3(512), 0, s,
-                         NB, NR, ntiles, nkt, Wf, asrc, epi);
+                         NB, NR, ntiles, nkt, Wf, asrc, epi, nullptr, nullptr);
   }
 }
 
@@ -1365,10 +1425,13 @@ static void launch_proj(int R, int ntiles, const float* Wf, const ASrc& asrc, co
 constexpr int FOLD_NT_BEAM = 2 * FOLD_NT;
 template <class ASrc, class Epi>
 static void launch_fold_gemm(int R, bool beam, int NB, int ntiles, const float* Wf, const ASrc& asrc, const Epi& epi,
-                             int s16, hipStream_t s) {
+                             int s16, hipStream_t s, f32x4* kspart = nullptr, int* kscnt = nullptr) {
   const int nkt = KPROJ / DG_BK;
   if (!beam) {  // (greedy: s16x3, or the exact-f32 MFMAs on the f32 fused image)
-    if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
+    // R <= 32 with a k-split buffer (CASR_OPT_DEC_KSPLIT): DG_KS blocks per 32 x 112 output block
+    if (R <= 32 && kspart && NB <= DG_KS_GROUPS && nkt % DG_KS == 0)
+      launch_dg<2, FOLD_NT, 3, 1, 1, false, 64, false, 3, DG_KS>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s, kspart, kscnt);
+    else if (R <= 32) launch_dg<2, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
     else launch_dg<4, FOLD_NT, 3>(NB, R, ntiles, nkt, Wf, asrc, epi, s16, s);
   } else if (dec_wide(R)) {  // (128 x 224 in two rounds at R = 2048 measured 12.07 against 11.47 ms per batch)
     // A ring of three beside the W ring of two (152 KB): fused GEMM 3.96-4.02 -> 3.88-3.92 ms per beam
@@ -1495,7 +1558,7 @@ static void fold_gemm_step(const DecodeArgs& a, DecodeBufs& d, int l, int total,
   if (!beam || a.V > 16 * GP_NT) gp.tmx = nullptr;  // tile maxima: beam only
   FoldEpi epi{a.W + a.L.proj_b, d.newdone, R, a.V, VT, l, total, d.err, gp, a.fb.gates, beam ? d.logits : nullptr, VG};
   dg_trace_step_gate(l, true, s);
-  launch_fold_gemm(R, beam, NB, ntiles, a.fb.wfold, asrc, epi, a.s16, s);
+  launch_fold_gemm(R, beam, NB, ntiles, a.fb.wfold, asrc, epi, a.s16, s, beam ? nullptr : reinterpret_cast<f32x4*>(d.kspart), d.kscnt);
   dg_trace_step_gate(l, false, s);
 }
 
@@ -1560,6 +1623,7 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
   fl.add32(out_len, 0, R);
   fl.add32(accum, 0, R);
   fl.add32(tokens, 0xffffffffu, (size_t)R * a.max_len);
+  if (d.kscnt) fl.add32(d.kscnt, 0, DG_KS_COUNTERS);
   hipError_t e0 = fill_multi(fl, s);
   if (e0 != hipSuccess) return e0;
   if (a.fold) return run_greedy_fold(a, d, tokens, out_len, finished, accum, align, s);

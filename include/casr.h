@@ -249,6 +249,12 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            cache lines (default, round 5; in effect with GEMM16_PERSIST = 2,
  *                            GEMM16_TAIL != 1 and KEYS_ROWS = 1, the forms that read it); 0: row
  *                            images.  The same words in another order: the same bits
+ *   CASR_OPT_DEC_KSPLIT      1: the greedy folded GEMM at R <= 32 decode rows (BASELINE config 2)
+ *                            splits its k range over 4 workgroups per 32 x 112 output block (252
+ *                            workgroups instead of 63; the 4 sums added in a fixed order by the last
+ *                            to arrive) (default, round 5); 0: one workgroup per output block.  The
+ *                            same products summed in another fixed order: tokens identical, scores
+ *                            within the stated tolerance
  * Two options select numerics variants instead (the same token ids, floating-point results within
  * the stated tolerances, not bit for bit; tests/test_gpu_parity.py compares each pair):
  *   CASR_OPT_ATTN_DIRECT     0: attention scores in the split exponential form 1 - 2 / (1 + e^{2k}
@@ -302,7 +308,8 @@ enum {
   CASR_OPT_LOGMEL_Q16 = 13,
   CASR_OPT_KEYS_ROWS = 14,
   CASR_OPT_X16_KM = 15,
-  CASR_OPT_COUNT = 16
+  CASR_OPT_DEC_KSPLIT = 16,
+  CASR_OPT_COUNT = 17
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

@@ -853,3 +853,45 @@ def test_odd_batches_greedy_match_oracle(eng, B):
     r = O.greedy_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd)
     assert toks == r["tokens"]
     np.testing.assert_allclose(score, r["score"], atol=2e-3, rtol=0)
+
+
+@pytest.mark.parametrize("B,graphs", [(1, False), (19, True), (32, False), (32, True)])
+def test_greedy_ksplit_small_batch(eng, B, graphs):
+    """BASELINE config 2's decode rows (R <= 32): the folded GEMM with its k range split over four
+    workgroups per output block (CASR_OPT_DEC_KSPLIT = 1, default; the last to arrive adds the four
+    sums in a fixed order) against one workgroup per output block: tokens identical, scores within
+    1e-4 (the same products summed in another order: 1.5e-5 measured on sums near -45), both equal to the CPU oracle's tokens, the
+    split path bitwise stable over repeated runs (graph replays included), and its arrival counters
+    left at zero (a second decode matches the first)."""
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    frames = [120] * (B - 1) + [57]
+    fb, fr = batch_fbank(frames, eng.device)
+    eng.encode_fbank(fb, fr)
+    eng.set_graphs(3 if graphs else 2)
+    res = {}
+    try:
+        for ks in (0, 1):
+            eng.set_option("DEC_KSPLIT", ks)
+            runs = []
+            for _ in range(3):
+                out = eng.greedy()
+                assert eng.device_flags() == 0
+                runs.append({k: v.cpu().clone() for k, v in out.items() if torch.is_tensor(v)})
+            for r2 in runs[1:]:
+                for k in runs[0]:
+                    assert torch.equal(runs[0][k], r2[k]), k
+            res[ks] = runs[0]
+    finally:
+        eng.set_option("DEC_KSPLIT", 1)
+        eng.set_graphs(2)
+    a, b = res[0], res[1]
+    assert torch.equal(a["tokens"], b["tokens"])
+    assert torch.equal(a["out_len"], b["out_len"])
+    np.testing.assert_allclose(b["accum"].numpy(), a["accum"].numpy(), atol=1e-4, rtol=0)
+    toks, score = greedy_outputs(b["tokens"].numpy(), b["out_len"].numpy(), b["finished"].numpy().astype(bool),
+                                 b["accum"].numpy())
+    feats = [O.features_from_fbank(fbank_for(i, t)) for i, t in enumerate(frames)]
+    r = O.greedy_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd)
+    assert toks == r["tokens"]
+    np.testing.assert_allclose(score, r["score"], atol=2e-3, rtol=0)
