@@ -249,14 +249,14 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            cache lines (default, round 5; in effect with GEMM16_PERSIST = 2,
  *                            GEMM16_TAIL != 1 and KEYS_ROWS = 1, the forms that read it); 0: row
  *                            images.  The same words in another order: the same bits
+ * Three options select numerics variants instead (the same token ids, floating-point results within
+ * the stated tolerances, not bit for bit; tests/test_gpu_parity.py compares each pair):
  *   CASR_OPT_DEC_KSPLIT      1: the greedy folded GEMM at R <= 32 decode rows (BASELINE config 2)
  *                            splits its k range over 4 workgroups per 32 x 112 output block (252
  *                            workgroups instead of 63; the 4 sums added in a fixed order by the last
  *                            to arrive) (default, round 5); 0: one workgroup per output block.  The
  *                            same products summed in another fixed order: tokens identical, scores
- *                            within the stated tolerance
- * Two options select numerics variants instead (the same token ids, floating-point results within
- * the stated tolerances, not bit for bit; tests/test_gpu_parity.py compares each pair):
+ *                            within 1e-4 of the unsplit form (test_greedy_ksplit_small_batch)
  *   CASR_OPT_ATTN_DIRECT     0: attention scores in the split exponential form 1 - 2 / (1 + e^{2k}
  *                            e^{2q}) (default; one transcendental per term); 1: the
  *                            direct tanh(k + q) form the split form falls back to per block
