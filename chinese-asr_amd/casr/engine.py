@@ -258,7 +258,8 @@ class Engine:
         return out, f
 
     def set_option(self, name, value):
-        """Tuning option (include/casr.h CASR_OPT_*, lib.OPTIONS): speed only, same bits."""
+        """Tuning option (include/casr.h CASR_OPT_*, lib.OPTIONS): speed only, same bits, except the
+        numerics variants ATTN_DIRECT, DEC_FOLD and DEC_KSPLIT (same tokens, results within tolerance)."""
         _lib.check(self.lib.casr_set_option(self.handle, _lib.OPTIONS[name], int(value)), self.handle)
 
     def get_option(self, name):
