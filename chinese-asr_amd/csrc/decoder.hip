@@ -1331,6 +1331,100 @@ __global__ void beam_finalize_kernel(int B, int k, int L, float lm_weight, float
   best_score[b] = bs;
 }
 
+// One wave per utterance (round 5): the same choice and walk as beam_finalize_kernel, with the
+// utterance's records, back-pointers and tokens staged in LDS first (one coalesced pass) and the
+// executed-step count from a wave prefix scan of newdone.  beam_finalize_kernel's thread per
+// utterance paid a memory round trip per back-pointer hop and per newdone word (68 us per beam
+// batch at B = 256, L = 40); here lane 0 walks LDS.  Same sequential order: the same bits.
+__global__ __launch_bounds__(64) void beam_finalize_wave_kernel(
+    int B, int k, int L, float lm_weight, float length_weight, const float* __restrict__ score0,
+    const float* __restrict__ score1, const int32_t* __restrict__ bp, const int32_t* __restrict__ tk,
+    const float* __restrict__ rec_score, const int32_t* __restrict__ rec_src, const uint8_t* __restrict__ rec_valid,
+    const int32_t* __restrict__ newdone, int32_t* __restrict__ best_tokens, int32_t* __restrict__ best_len,
+    float* __restrict__ best_score, int32_t* __restrict__ steps_out, int32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) int32_t fsm[];
+  const int b = blockIdx.x, ln = threadIdx.x, R = B * k, LK = L * k;
+  int32_t* sbp = fsm;
+  int32_t* stk = sbp + LK;
+  float* srs = reinterpret_cast<float*>(stk + LK);
+  uint8_t* srv = reinterpret_cast<uint8_t*>(srs + LK);
+  // executed_steps(): the first s whose running sum of newdone reaches B (else L)
+  int steps = L, carry = 0;
+  for (int s0 = 0; s0 < L; s0 += 64) {
+    const int sl = s0 + ln;
+    int v = sl < L ? newdone[sl] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(v, o);
+      if (ln >= o) v += t;
+    }
+    v += carry;
+    const unsigned long long hit = __ballot(sl < L && v >= B);
+    if (hit) {
+      steps = s0 + __ffsll((long long)hit);
+      break;
+    }
+    carry = __shfl(v, 63);
+  }
+  if (b == 0 && ln == 0) steps_out[0] = steps;
+  const int n = steps * k;
+  for (int i = ln; i < n; i += 64) {
+    const int st = i / k, c = i - st * k;
+    sbp[i] = bp[(size_t)st * R + b * k + c];
+    stk[i] = tk[(size_t)st * R + b * k + c];
+    srs[i] = rec_score[(size_t)b * LK + i];
+    srv[i] = rec_valid[(size_t)b * LK + i];
+  }
+  __syncthreads();
+  int len = 0;
+  if (ln == 0) {
+    const float* score_final = (steps & 1) ? score1 : score0;
+    int bl = -1, bc = -1;
+    float bs = 0.f;
+    for (int i = 0; i < n; ++i)
+      if (srv[i] && (bl < 0 || srs[i] > bs)) {
+        bl = i / k;
+        bc = i - bl * k;
+        bs = srs[i];
+      }
+    int32_t* out = best_tokens + (size_t)b * L;
+    int slot, from;
+    if (bl >= 0) {
+      len = bl;
+      slot = rec_src[((size_t)b * L + bl) * k + bc];
+      from = bl - 1;
+    } else {
+      const int ll = steps - 1;
+      const float lw = (float)((double)length_weight * (double)(ll + 1));
+      int bj = 0;
+      float bsv = 0.f;
+      for (int j = 0; j < k; ++j) {
+        const float sv = (score_final[b * k + j] + lm_weight * 0.f) + lw;
+        if (j == 0 || sv > bsv) {
+          bsv = sv;
+          bj = j;
+        }
+      }
+      bs = bsv;
+      len = ll + 1;
+      slot = bj;
+      from = ll;
+    }
+    for (int st = from; st >= 0; --st) {
+      if ((unsigned)slot >= (unsigned)k) {
+        atomicOr(err, CASR_DEV_BAD_BACKPTR);
+        slot = 0;
+      }
+      out[st] = stk[st * k + slot];
+      slot = sbp[st * k + slot];
+    }
+    best_len[b] = len;
+    best_score[b] = bs;
+  }
+  len = __shfl(len, 0);
+  for (int st = len + ln; st < L; st += 64) best_tokens[(size_t)b * L + st] = -1;
+}
+
 // grid (B, L), block 64: expand every finished record's token sequence.
 __global__ void beam_records_kernel(int B, int k, int L, const int32_t* __restrict__ bp,
                                     const int32_t* __restrict__ tk, const float* __restrict__ rec_score,
@@ -1704,9 +1798,15 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
     else if (a.k <= 8) launch_beam_select<16>(a, d, l, s);
     else launch_beam_select<32>(a, d, l, s);
   }
-  hipLaunchKernelGGL(beam_finalize_kernel, dim3((a.B + 63) / 64), dim3(64), 0, s, a.B, a.k, a.max_len,
-                     lm_weight, length_weight, d.score[0], d.score[1], d.bp, d.tk, d.rec_score, d.rec_src,
-                     d.rec_valid, d.newdone, best_tokens, best_len, best_score, steps, d.err);
+  const size_t fin_lds = (size_t)a.max_len * a.k * (3 * sizeof(int32_t) + 1) + 16;
+  if (fin_lds <= 64 * 1024)
+    hipLaunchKernelGGL(beam_finalize_wave_kernel, dim3(a.B), dim3(64), fin_lds, s, a.B, a.k, a.max_len,
+                       lm_weight, length_weight, d.score[0], d.score[1], d.bp, d.tk, d.rec_score, d.rec_src,
+                       d.rec_valid, d.newdone, best_tokens, best_len, best_score, steps, d.err);
+  else  // (a max_len x k past the LDS: the thread-per-utterance form)
+    hipLaunchKernelGGL(beam_finalize_kernel, dim3((a.B + 63) / 64), dim3(64), 0, s, a.B, a.k, a.max_len,
+                       lm_weight, length_weight, d.score[0], d.score[1], d.bp, d.tk, d.rec_score, d.rec_src,
+                       d.rec_valid, d.newdone, best_tokens, best_len, best_score, steps, d.err);
   return hipGetLastError();
 }
 

@@ -21,9 +21,9 @@ from collections import defaultdict
 # and half-tile tail together; None = one launch per dispatch, counted: the folded decode step
 #  launches the LSTMCell GEMM once per decode and its fused GEMM is the proj class)
 CLASS_OF = {
-    "input_proj": (("gemm16_persist_kernel", "gemm16_bias_kernel"), 4),
+    "input_proj": (("gemm16_persist_kernel", "gemm16_bias_kernel", "gemm16_pp_kernel", "gemm16_tail_kernel"), 4),
     "rec_step": (("rec_layer_kernel",), 4),
-    "keys": (("gemm_nt_kernel<KeysEpi",), 1),
+    "keys": (("gemm_nt_kernel<KeysEpi", "keys16_kernel"), 1),
     "dec_lstm": (("dgemm_kernel<*DecLstmA",), None),
     "proj": (("dgemm_kernel<*ProjA",), None),
     "select": (("beam_select_kernel",), None),
