@@ -1343,11 +1343,11 @@ __global__ __launch_bounds__(64) void beam_finalize_wave_kernel(
     const int32_t* __restrict__ newdone, int32_t* __restrict__ best_tokens, int32_t* __restrict__ best_len,
     float* __restrict__ best_score, int32_t* __restrict__ steps_out, int32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) int32_t fsm[];
-  const int b = blockIdx.x, ln = threadIdx.x, R = B * k, LK = L * k;
+  const int b = blockIdx.x, ln = threadIdx.x, R = B * k, LK = L * k, LKp = (LK + 7) & ~7;
   int32_t* sbp = fsm;
-  int32_t* stk = sbp + LK;
-  float* srs = reinterpret_cast<float*>(stk + LK);
-  uint8_t* srv = reinterpret_cast<uint8_t*>(srs + LK);
+  int32_t* stk = sbp + LKp;
+  float* srs = reinterpret_cast<float*>(stk + LKp);
+  uint8_t* srv = reinterpret_cast<uint8_t*>(srs + LKp);
   // executed_steps(): the first s whose running sum of newdone reaches B (else L)
   int steps = L, carry = 0;
   for (int s0 = 0; s0 < L; s0 += 64) {
@@ -1375,18 +1375,29 @@ __global__ __launch_bounds__(64) void beam_finalize_wave_kernel(
     srs[i] = rec_score[(size_t)b * LK + i];
     srv[i] = rec_valid[(size_t)b * LK + i];
   }
+  for (int i = n + ln; i < ((n + 7) & ~7); i += 64) srv[i] = 0;  // the scan reads 8 at a time
   __syncthreads();
   int len = 0;
   if (ln == 0) {
     const float* score_final = (steps & 1) ? score1 : score0;
     int bl = -1, bc = -1;
     float bs = 0.f;
-    for (int i = 0; i < n; ++i)
-      if (srv[i] && (bl < 0 || srs[i] > bs)) {
-        bl = i / k;
-        bc = i - bl * k;
-        bs = srs[i];
+    // records in (step, slot) order, 8 per LDS round trip, compared in that order
+    for (int i0 = 0; i0 < n; i0 += 8) {
+      const uint2 v8 = *reinterpret_cast<const uint2*>(srv + i0);
+      const float4 s0 = *reinterpret_cast<const float4*>(srs + i0);
+      const float4 s1 = *reinterpret_cast<const float4*>(srs + i0 + 4);
+      const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool valid = ((e < 4 ? v8.x : v8.y) >> (8 * (e & 3))) & 0xFFu;
+        if (valid && (bl < 0 || sv[e] > bs)) {
+          bl = (i0 + e) / k;
+          bc = (i0 + e) - bl * k;
+          bs = sv[e];
+        }
       }
+    }
     int32_t* out = best_tokens + (size_t)b * L;
     int slot, from;
     if (bl >= 0) {
@@ -1798,7 +1809,7 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
     else if (a.k <= 8) launch_beam_select<16>(a, d, l, s);
     else launch_beam_select<32>(a, d, l, s);
   }
-  const size_t fin_lds = (size_t)a.max_len * a.k * (3 * sizeof(int32_t) + 1) + 16;
+  const size_t fin_lds = (size_t)((a.max_len * a.k + 7) & ~7) * (3 * sizeof(int32_t) + 1) + 16;
   if (fin_lds <= 64 * 1024)
     hipLaunchKernelGGL(beam_finalize_wave_kernel, dim3(a.B), dim3(64), fin_lds, s, a.B, a.k, a.max_len,
                        lm_weight, length_weight, d.score[0], d.score[1], d.bp, d.tk, d.rec_score, d.rec_src,
