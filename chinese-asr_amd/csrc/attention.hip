@@ -120,6 +120,11 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   static_assert(CELL != 1 || KPB == 1, "the folded greedy step: one row per block");
   static_assert(CELL != 2 || KPB >= 2, "the folded beam step: beam rows of one utterance per block");
   static_assert(CELL != 3 || KPB == 4 || KPB == 8, "the fused beam select: one block per utterance, k = 4 or 8");
+  static_assert(CELL != 4 || KPB == 4, "the fused beam select, two blocks per utterance: k = 8");
+  // CELL 4 (round 5): KPB 4 at k = 8, so two blocks per utterance (B = 128: 256 blocks) run the same
+  // select of step l - 1; the first (blockIdx.y == 0) does its global bookkeeping, both read their
+  // rows' tokens and predecessor rows from their own copy
+  constexpr int KSEL = CELL == 4 ? 2 * KPB : KPB;  // rows of the fused select
   extern __shared__ __attribute__((aligned(16))) float sm[];
   uint32_t* atr = g_at_trace ? g_at_trace + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 : nullptr;
   auto stamp = [&](int i) {
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   // (CELL 1: the early exit is decided after the block's own select, below.  CELL 3: the select of
   // step l - 1 skips when every utterance finished before step l - 1; otherwise the block runs it and
   // the attention, whatever this launch's selects add to step l - 1's count)
-  if (CELL != 1 && done_before(newdone, CELL == 3 ? l - 1 : l) >= total) return;
+  if (CELL != 1 && done_before(newdone, CELL >= 3 ? l - 1 : l) >= total) return;
   const int Tq = attn_tq(Tp);
   float* qs = sm;                   // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
   float* eqs = qs + KPB * AT_APAD;  // [AT_APAD][KPB]: exp(2q) (split form), zero past A
@@ -336,17 +341,18 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     // (CELL 3) the beam select of step l - 1 for utterance b, in the score scratch (free until the
     // scores); its tokens and predecessor rows also go to bs_tok / bs_src, prefilled with what
     // tok / src hold, as the separate launch leaves slots no candidate fills
-    __shared__ int bs_tok[CELL == 3 ? KPB : 1], bs_src[CELL == 3 ? KPB : 1];
-    if constexpr (CELL == 3) {
-      using SelLds = BeamSelLds<2 * KPB, KPB, AT_WAVES>;
+    __shared__ int bs_tok[CELL >= 3 ? KSEL : 1], bs_src[CELL >= 3 ? KSEL : 1];
+    if constexpr (CELL >= 3) {
+      using SelLds = BeamSelLds<2 * KSEL, KSEL, AT_WAVES>;
       static_assert(sizeof(SelLds) <= attn_scratch_floats<KPB>(4) * sizeof(float), "the select's LDS fits the scratch");
-      if (tid < KPB) {
-        bs_tok[tid] = cell.bs.tok_next[row0 + tid];
-        bs_src[tid] = cell.bs.src_next[row0 + tid];
+      if (tid < KSEL) {
+        bs_tok[tid] = cell.bs.tok_next[(size_t)b * k + tid];
+        bs_src[tid] = cell.bs.src_next[(size_t)b * k + tid];
       }
       SelLds& sl = *reinterpret_cast<SelLds*>(xs);
-      if (cell.bs.temperature == 1.0f) beam_select_block<2 * KPB, true>(cell.bs, b, sl, nullptr, bs_tok, bs_src);
-      else beam_select_block<2 * KPB, false>(cell.bs, b, sl, nullptr, bs_tok, bs_src);
+      const bool writer = CELL == 3 || blockIdx.y == 0;
+      if (cell.bs.temperature == 1.0f) beam_select_block<2 * KSEL, true>(cell.bs, b, sl, nullptr, bs_tok, bs_src, writer);
+      else beam_select_block<2 * KSEL, false>(cell.bs, b, sl, nullptr, bs_tok, bs_src, writer);
       __syncthreads();  // bs_tok / bs_src written; the scratch is free again
       stamp(6);
     }
@@ -366,9 +372,9 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     for (int j = 0; j < KPB; ++j) {
       const int r = (int)row0 + min(j, nk - 1);
       int sj, tj;
-      if constexpr (CELL == 3) {
-        sj = bs_src[min(j, nk - 1)];
-        tj = bs_tok[min(j, nk - 1)];
+      if constexpr (CELL >= 3) {
+        sj = bs_src[j0 + min(j, nk - 1)];
+        tj = bs_tok[j0 + min(j, nk - 1)];
       } else {
         sj = cell.src[r];
         tj = cell.tok[r];
@@ -836,7 +842,10 @@ hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const Attn
   if (a.k == 1) return launch_kpb<1, 1>(a, st, nullptr, align, newdone, l, total, s, cell);
   switch (attention_kpb(a.B, a.k, a.attn_kpb)) {
     case 4:
-      if (cell.bsel) return a.k == 4 ? launch_kpb<4, 3>(a, st, nullptr, align, newdone, l, total, s, cell) : hipErrorInvalidValue;
+      if (cell.bsel)
+        return a.k == 4 ? launch_kpb<4, 3>(a, st, nullptr, align, newdone, l, total, s, cell)
+               : a.k == 8 ? launch_kpb<4, 4>(a, st, nullptr, align, newdone, l, total, s, cell)
+                          : hipErrorInvalidValue;
       return launch_kpb<4, 2>(a, st, nullptr, align, newdone, l, total, s, cell);
     case 8:
       if (cell.bsel) return a.k == 8 ? launch_kpb<8, 3>(a, st, nullptr, align, newdone, l, total, s, cell) : hipErrorInvalidValue;

@@ -103,10 +103,13 @@ struct BeamSelLds {
 // the caller has checked the early exit (done_before(newdone, l) < B).  tok_l / src_l (or null):
 // the block's LDS copy of the tokens and predecessor rows it writes to tok_next / src_next (slots
 // no candidate fills keep what the caller put there).  No barrier after the bookkeeping: a caller
-// that reads S, tok_l or src_l afterwards synchronises first.
+// that reads S, tok_l or src_l afterwards synchronises first.  writer = false (the second of two
+// blocks that run the same select, attention.hip CELL 4): the same choice into tok_l / src_l, no
+// global bookkeeping (its finished-count increment must happen once).
 template <int K2, bool UNIT_T, int NR, int NWV>
 __device__ __forceinline__ void beam_select_block(const BeamSelArgs& a, int b, BeamSelLds<K2, NR, NWV>& S,
-                                                  uint32_t* btr, int32_t* tok_l, int32_t* src_l) {
+                                                  uint32_t* btr, int32_t* tok_l, int32_t* src_l,
+                                                  bool writer = true) {
   constexpr int NTH = 64 * NWV;
   const float* __restrict__ logits = a.logits;
   const int V = a.V, B = a.B, k = a.k, l = a.l, L = a.L, eos = a.eos;
@@ -533,7 +536,7 @@ __device__ __forceinline__ void beam_select_block(const BeamSelArgs& a, int b, B
     const int beam = cc / V, tok = cc - beam * V;
     const bool f = inr && tok == eos;
     const float cs = inr ? S.cv[c] : 0.f;
-    if (c < k) {  // finished hypotheses among the first k candidates (model.py:874-889)
+    if (writer && c < k) {  // finished hypotheses among the first k candidates (model.py:874-889)
       const size_t ri = ((size_t)b * L + l) * k + c;
       a.rec_valid[ri] = f;
       if (f) {
@@ -541,7 +544,7 @@ __device__ __forceinline__ void beam_select_block(const BeamSelArgs& a, int b, B
         a.rec_src[ri] = beam;
       }
     }
-    if (ln == 0 && !a.topfin[b] && tok == eos) {  // model.py:897-901 (candidate 0)
+    if (writer && ln == 0 && !a.topfin[b] && tok == eos) {  // model.py:897-901 (candidate 0)
       a.topfin[b] = 1;
       atomicAdd(&a.newdone[l], 1);
     }
@@ -551,15 +554,17 @@ __device__ __forceinline__ void beam_select_block(const BeamSelArgs& a, int b, B
     const int slot = f ? __popcll(ne) + __popcll(eo & below) : __popcll(ne & below);
     if (inr && slot < k) {
       const int row = b * k + slot;
-      a.tok_next[row] = tok;
-      a.src_next[row] = b * k + beam;
-      if (tok_l) {  // the fused caller's copy (attention.hip CELL 3)
+      if (tok_l) {  // the fused caller's copy (attention.hip CELL 3, 4)
         tok_l[slot] = tok;
         src_l[slot] = b * k + beam;
       }
-      a.score_next[row] = cs;
-      a.bp[(size_t)l * R + row] = beam;
-      a.tk[(size_t)l * R + row] = tok;
+      if (writer) {
+        a.tok_next[row] = tok;
+        a.src_next[row] = b * k + beam;
+        a.score_next[row] = cs;
+        a.bp[(size_t)l * R + row] = beam;
+        a.tk[(size_t)l * R + row] = tok;
+      }
     }
     stamp(6, (uint32_t)__builtin_amdgcn_s_memrealtime());
   }

@@ -1787,7 +1787,9 @@ hipError_t run_beam(const DecodeArgs& a, DecodeBufs& d, float lm_weight, float l
   // the folded step with one attention block per utterance (k = 4 or 8 rows per block): the select
   // of step l - 1 runs in step l's attention prologue (CASR_OPT_FUSE_SELECT; the last step's select
   // is a launch of its own)
-  const bool fsel = a.fold && a.fuse_select && (a.k == 4 || a.k == 8) && attention_kpb(a.B, a.k, a.attn_kpb) == a.k;
+  // (k = 8 at 4 rows per attention block: both blocks of an utterance run the select, CELL 4)
+  const int fkpb = attention_kpb(a.B, a.k, a.attn_kpb);
+  const bool fsel = a.fold && a.fuse_select && (a.k == 4 || a.k == 8) && (fkpb == a.k || (a.k == 8 && fkpb == 4));
   for (int l = 0; l < a.max_len; ++l) {
     // the folded step (CASR_OPT_DEC_FOLD): step 0's LSTMCell + attention, then per step the
     // attention with the cell prologue (l >= 1) and the fused GEMM

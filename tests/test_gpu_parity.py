@@ -267,8 +267,9 @@ def test_fused_select_equals_select_launches(eng, eos_bias, graphs):
         assert bool(outs[1]["finished"].any()), "with the EOS bias some rows must finish early"
 
 
-@pytest.mark.parametrize("k,eos_bias,graphs", [(8, 0.0, False), (8, 12.0, True), (8, 40.0, False), (4, 40.0, True)])
-def test_beam_select_in_attention_equals_select_launches(eng, k, eos_bias, graphs):
+@pytest.mark.parametrize("k,eos_bias,graphs,B", [(8, 0.0, False, 256), (8, 12.0, True, 256), (8, 40.0, False, 256),
+                                                 (4, 40.0, True, 256), (8, 0.0, False, 128), (8, 40.0, True, 128)])
+def test_beam_select_in_attention_equals_select_launches(eng, k, eos_bias, graphs, B):
     """The folded beam step with one attention block per utterance (k = 4 or 8 at B = 256, R >= 1024
     rows): the select of step l - 1 run in step l's attention prologue (default, attention.hip CELL 3)
     and every select a launch of its own (CASR_OPT_FUSE_SELECT = 0) give the same tokens, lengths,
@@ -277,12 +278,12 @@ def test_beam_select_in_attention_equals_select_launches(eng, k, eos_bias, graph
     (eos_bias 40: every utterance's top candidate ends early, so the fused attention of the step after
     the last select runs on counters it cannot know complete).  Without graphs: the folded step is in
     effect (one LSTMCell launch, step 0's) and the fused decode launches one select (the last step's)
-    instead of one per step."""
+    instead of one per step.  B = 128, k = 8 (4 rows per attention block, CELL 4): both blocks of an
+    utterance run its select, the first one writes the bookkeeping."""
     if eng.requested != "s16x3":
         pytest.skip("the beam fold, and with it the fused select, runs on the s16x3 images")
     enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True, eos_bias=eos_bias)
     eng.bind(pack_weights(CFG, enc_sd, dec_sd))
-    B = 256
     rs = np.random.RandomState(9)
     frames = rs.randint(30, 300, size=B)
     x = np.zeros((B, 300, 80), np.float32)
