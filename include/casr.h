@@ -215,8 +215,10 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  * keys of the captured hipGraphs, so changing one between calls takes effect at the next call.
  *   CASR_OPT_FUSE_SELECT     1 (default): the select of step l runs inside a kernel of step l + 1:
  *                            greedy, the LSTMCell (three-launch step) or the attention (folded
- *                            step); beam 4 or 8 with one attention block per utterance (folded
- *                            step), the attention.  0: every select a launch of its own
+ *                            step); beam 4 or 8 with one attention block per utterance, or beam 8
+ *                            with two (4 rows per block: both run the select, the first writes the
+ *                            bookkeeping) (folded step), the attention.  0: every select a launch
+ *                            of its own
  *   CASR_OPT_REC_LAYOUT      persistent recurrence workgroup shape: 0 auto (default: 16 rows x 16
  *                            units when that grid fits one workgroup per CU, else 32 x 16), 1 32x16,
  *                            2 16x32, 3 16x16
