@@ -64,6 +64,13 @@ typedef float ks_f2 __attribute__((ext_vector_type(2)));  // (the k split's 8-by
 // (round 5) the projection epilogue's row partials take exp(x - max) as v_exp_f32 of (x - max)
 // log2(e) instead of the libm expf (about 15 instructions each, 7 x 16 per lane and block in the beam
 // shape); 0 restores expf (diagnostic builds, tools/probes/ab_libs.sh)
+// (round 5) the beam logits rows go out with the non-temporal hint: the select re-reads only the
+// few tiles that can hold a top-2k candidate (about 16 of 313 per row), so the 41 MB per step need
+// no cache residency (three interleaved rounds: beam fused GEMM 3.61-3.63 -> 3.54-3.55 ms per beam
+// batch, profiles/r05/logits_nt/); 0 restores plain stores (diagnostic builds)
+#ifndef CASR_LOGITS_NT
+#define CASR_LOGITS_NT 1
+#endif
 #ifndef CASR_FAST_PART_EXP
 #define CASR_FAST_PART_EXP 1
 #endif
@@ -827,7 +834,11 @@ __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const f
     if (row < R) {
       float* dst = logits + (size_t)row * V + col;
       if (vec && col + 3 < V) {
+#if CASR_LOGITS_NT
+        __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(dst));
+#else
         *reinterpret_cast<float4*>(dst) = v;
+#endif
       } else {
         if (col < V) dst[0] = v.x;
         if (col + 1 < V) dst[1] = v.y;

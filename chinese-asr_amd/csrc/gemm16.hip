@@ -390,6 +390,14 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
 //     issues 32 stores and the vmcnt counts stay exact); one barrier, then the next tile's region.
 // Arithmetic: per accumulator the same MFMAs in the same k order as gemm16_persist_kernel (16-deep
 // stage j = k-step j & 1 of 32-deep tile j >> 1), so the outputs are bitwise equal.
+// (round 5) the input projection's Gin rows (557 MB per layer at B = 256, each read once by the
+// recurrence) go out with the non-temporal hint, so they do not displace what the caches hold for
+// the recurrence and the next GEMM (three interleaved rounds, profiles/r05/gin_nt/: greedy batch
+// 6.69-6.72 -> 6.59-6.60 ms, beam 10.65-10.75 -> 10.50-10.57 ms, the recurrence class the one that
+// moves); 0 restores plain stores (diagnostic builds)
+#ifndef CASR_GIN_NT
+#define CASR_GIN_NT 1
+#endif
 constexpr int PP_ROWF = 16;                  // floats per staged row (64 B)
 constexpr int PP_OP = G16_M * PP_ROWF;       // floats per operand and stage (16 KB)
 constexpr int PP_STAGE = 2 * PP_OP;          // [A | W]
@@ -604,7 +612,8 @@ __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restri
             const int lr = wm * 128 + tm * 32 + 16 * hh + row;  // row within the tile
             const float4 o = make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
             if (!(DIAG & 4))
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, (lr * N + cbase) * 4, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, (lr * N + cbase) * 4, 0,
+                                                     CASR_GIN_NT ? 2 : 0);
             else if (v.x == 12345.f)
               Cout[0] = o.x;
           }
@@ -755,8 +764,11 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
       const int gr = m0 + tm * 32 + row;
       if (gr < M) {
         const float4 v = *reinterpret_cast<const float4*>(ring + row * LDC + c4 * 4);
-        *reinterpret_cast<float4*>(Cout + (size_t)gr * N + n0 + c4 * 4) =
-            make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
+        const float4 o4 = make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
+        if (CASR_GIN_NT)
+          __builtin_nontemporal_store(f32x4{o4.x, o4.y, o4.z, o4.w}, reinterpret_cast<f32x4*>(Cout + (size_t)gr * N + n0 + c4 * 4));
+        else
+          *reinterpret_cast<float4*>(Cout + (size_t)gr * N + n0 + c4 * 4) = o4;
       }
     }
   }
