@@ -115,25 +115,13 @@ def kernel_bytes(cls, B, Tp, R, V, fold=False, s16=True):
 
 class _StubLM:
     """Deterministic stand-in for kenlm.LanguageModel.score (main.py:82, model.py:755): KenLM and
-    an LM file are absent offline.  Tokens arrive as private-use characters (id -> U+E000 + id)."""
-
-    def __init__(self):
-        self._r = {}  # word -> its id % 97 (filled on first sight)
+    an LM file are absent offline.  Tokens arrive as private-use characters (id -> U+E000 + id).
+    Every call does its own work (no per-word cache), so the host part of config 5 keeps the
+    per-hypothesis cost pattern of a real LM call (tests/golden/stub_lm.py, the same function)."""
 
     def score(self, s, bos=True):
-        # -0.37 n - 0.011 sum(id % 97) - 0.5 bos over the words' ids (the same integer sum and float
-        # operations as the per-call form, with each word's term looked up once it has been seen)
-        ws = s.split(" ")
-        if "" in ws:
-            ws = [w for w in ws if w]
-        r = self._r
-        try:
-            tot = sum(map(r.__getitem__, ws))
-        except KeyError:
-            for w in ws:
-                r.setdefault(w, (ord(w) - 0xE000) % 97)
-            tot = sum(map(r.__getitem__, ws))
-        return -0.37 * len(ws) - 0.011 * tot - (0.5 if bos else 0.0)
+        ids = [ord(w) - 0xE000 for w in s.split(" ") if w]
+        return -0.37 * len(ids) - 0.011 * sum(i % 97 for i in ids) - (0.5 if bos else 0.0)
 
 
 # CPU port vs the reference itself on the same 8 container cores (tools/calibrate_cpu.py, committed
@@ -217,6 +205,8 @@ def main():
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the BASELINE config 1 (one WAV via main.parse), config 2 (B=32 greedy) and "
                          "config 5 (beam 16 + LM) side lines")
+    ap.add_argument("--sharded-batch", type=int, default=1024,
+                    help="global batch of the BASELINE config 4 / 5 lines (partitioned over the ranks)")
     ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--cpu-beam-sample", type=int, default=64)
     ap.add_argument("--precision", default="s16x3", choices=["s16x3", "f32"],
@@ -465,78 +455,75 @@ def main():
                   "unit": "utt/s", "chars": len(text)}
         del m1
 
-    # BASELINE config 5: beam 16 + second-pass LM rescoring, B = 128 per GPU (1024 on 8 GPUs).
-    # Weights with the EOS bias of the peaked recipe so hypotheses finish and the second pass has
-    # candidates to rescore; KenLM is absent offline, so the LM is a deterministic stub scored on
-    # the host (the reference also scores on the host, model.py:749-763).  Timed: features,
-    # encoder, beam decode, the finished-hypothesis records to the host and the rescoring.
-    lm_line = None
-    if not args.no_configs:
-        from casr.results import second_pass_arrays
-        Bl, kl = args.config3_batch, 16
-        eng5 = Engine(cfg, *synthetic_state_dicts(cfg, peaked=True), device=dev)
-        eng5.set_precision(args.precision)
-        fbl = torch.from_numpy(fbank_batch(rank * Bl, Bl, T)).to(dev)
-        frl = torch.full((Bl,), T, dtype=torch.int32, device=dev)
-        i2w = {i: chr(0xE000 + i) for i in range(cfg.vocab)}
-        lm = _StubLM()
-        info = {}
+    # BASELINE configs 4 and 5 through the product's sharded call (casr.distributed.decode_sharded):
+    # a global batch of --sharded-batch (1,024) utterances is partitioned over the world's ranks
+    # (128 per GPU at --gpus 8, all 1,024 on one GPU at --gpus 1: fixed total work, "strong"), each
+    # rank decodes its shard (BeamShardDecoder: features, encoder, beam; config 5 also the records to
+    # the host and the second pass there) and the results are gathered as arrays onto every rank --
+    # the gather is inside the timed region.  Config 5 uses the weights with the EOS bias (so
+    # hypotheses finish and the second pass has records to rescore) and a deterministic stub LM
+    # called once per hypothesis (KenLM and an LM file are absent offline; the reference also
+    # scores on the host, model.py:749-763); its host part is reported beside the line.
+    sharded = {}
+    if not args.no_configs and args.sharded_batch > 0:
+        from casr.distributed import BeamShardDecoder, decode_sharded, partition
+        G = args.sharded_batch
+        lens_g = [T // 3] * G
+        my_idx = partition(lens_g, world)[rank]
+        fb_sh = torch.from_numpy(np.stack([fbank_batch(int(i), 1, T)[0] for i in my_idx])).to(dev)
+        fr_sh = torch.full((len(my_idx),), T, dtype=torch.int32, device=dev)
+        gdev = dev if world > 1 else None
+        names = [d.replace(" ", "_") for d in [torch.cuda.get_device_name(dev)]]
+        dev_names = [None] * world
+        if dist is not None:
+            dist.all_gather_object(dev_names, (rank, names[0]))
+        else:
+            dev_names = [(0, names[0])]
+        for tag, kk, lm_on in (("config4", args.beam, False), ("config5", 16, True)):
+            e_sh = eng if not lm_on else Engine(cfg, *synthetic_state_dicts(cfg, peaked=True), device=dev)
+            e_sh.set_precision(args.precision)
+            lm = _StubLM() if lm_on else None
+            dec = BeamShardDecoder(e_sh, kk, lm, {i: chr(0xE000 + i) for i in range(cfg.vocab)} if lm_on else None,
+                                   1.5 if lm_on else 0.0, 1.5 if lm_on else 0.0)
+            batches = lambda n: [(lens_g, lambda idx: (fb_sh, fr_sh))] * n
+            for out in decode_sharded(batches(2), dec, device=gdev):
+                pass
+            flags[tag + "_warmup"] = e_sh.device_flags()
+            nb = args.beam_steps
+            gc.collect()
+            gc.freeze()  # a serving process freezes its start-up heap (tools/probes/config5_probe.py)
+            t_host = [0.0]
+            fin = dec.finish
 
-        # Serving loop: batch i's device work (features, encoder, beam, records) is enqueued and
-        # its records copied into one of two pinned host buffers; the host then rescores batch
-        # i-1 while the GPU runs batch i.  Every batch is fully processed inside the timed
-        # region (the last one is drained before the clock stops).
-        pinned = [None, None]
-
-        def enqueue(slot):
-            eng5.encode_fbank(fbl, frl)
-            r = eng5.beam(kl, 1.5, 1.5)
-            dev_out = (r["tokens"], r["length"], r["steps"]) + tuple(eng5.beam_records())
-            if pinned[slot] is None:
-                pinned[slot] = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in dev_out]
-            for h, x in zip(pinned[slot], dev_out):
-                h.copy_(x, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            return slot, ev
-
-        def finish(pend):
-            slot, ev = pend
-            ev.synchronize()
-            # one sequential copy out of the pinned (possibly uncached) buffers, then the gathers
-            toks, blen, steps, rt, rs, rv = (h.numpy().copy() for h in pinned[slot])
-            best = {b: (toks[b, :blen[b]].tolist(), 0.0) for b in range(Bl)}
-            best.update(second_pass_arrays(rt, rs, rv, i2w, lm, 1.5, 1.5))
-            info["steps"] = int(steps[0])
-            nrec = np.bincount(np.nonzero(rv)[0], minlength=Bl)
-            info["rescored"] = int(np.count_nonzero(nrec > 1))
-            return best
-
-        def run_lm(n):
-            prev = None
-            for i in range(n):
-                cur = enqueue(i % 2)
-                if prev is not None:
-                    finish(prev)
-                prev = cur
-            return finish(prev)
-
-        run_lm(2)
-        # a serving process freezes its start-up heap: the host rescoring allocates ~10^5 small
-        # objects per batch, and each full cyclic-GC pass over the torch / numpy heap otherwise
-        # adds ~50 ms to the batch it lands in (measured, tools/probes/config5_probe.py)
-        gc.collect()
-        gc.freeze()
-        dtl = timed(lambda: run_lm(args.beam_steps), 1, "config5", e=eng5)
-        gc.unfreeze()
-        lm_line = {"config": "BASELINE config 5: beam 16 + second-pass LM rescoring (stub LM, host)",
-                   "k": kl, "batch_per_gpu": Bl, "value": Bl * world * args.beam_steps / dtl, "unit": "utt/s",
-                   "ms_per_step": 1000.0 * dtl / args.beam_steps, "decode_steps": info.get("steps"),
-                   "utterances_rescored": info.get("rescored"),
-                   "weights": "synthetic recipe with the EOS bias (hypotheses finish before step 40)",
-                   "pipelined": "host rescoring of batch i-1 overlaps the device work of batch i "
-                                "(records double-buffered in pinned host memory)"}
-        eng5.close()
+            def timed_finish(pend, fin=fin):
+                t0 = time.perf_counter()
+                r = fin(pend)
+                t_host[0] += time.perf_counter() - t0
+                return r
+            dec.finish = timed_finish
+            dts = timed(lambda: [None for _ in decode_sharded(batches(nb), dec, device=gdev)], 1, tag, e=e_sh)
+            gc.unfreeze()
+            line = {"config": ("BASELINE config 4: beam 8" if not lm_on else
+                               "BASELINE config 5: beam 16 + second-pass LM rescoring (stub LM, host)") +
+                              f", {G} utterances sharded over {world} GPU(s), T={T}",
+                    "k": kk, "global_batch": G, "batch_per_gpu": len(my_idx), "world_size": world,
+                    "devices": [n for _, n in sorted(dev_names)], "batches": nb,
+                    "value": G * nb / dts, "unit": "utt/s", "ms_per_batch": 1000.0 * dts / nb,
+                    "rtf": dts / nb / (G * AUDIO_S_PER_UTT), "scaling": "strong",
+                    "decode_steps": dec.stats.get("steps"),
+                    "entry_point": "casr.distributed.decode_sharded (partition -> BeamShardDecoder -> gather_arrays); "
+                                   "the gather is inside the timed region",
+                    "pipelined": "two global batches in flight: batch i's device work is enqueued before "
+                                 "batch i-1's host part and gather",
+                    "host_ms_per_batch_rank0": 1000.0 * t_host[0] / nb}
+            if lm_on:
+                line.update(records_per_batch_rank0=dec.stats.get("records"),
+                            weights="synthetic recipe with the EOS bias (hypotheses finish before step 40)",
+                            lm="deterministic stub, one call per hypothesis of every utterance with > 1 "
+                               "(the reference's call pattern, model.py:755); a KenLM call costs more")
+            sharded[tag] = line
+            if lm_on:
+                e_sh.close()
 
     # side measurement: the same greedy step on the exact-f32 MFMA path (not the headline)
     f32_cmp = None
@@ -596,7 +583,8 @@ def main():
                                          "the committed PMC passes (profiles/pmc_traffic.json)"},
             "config2_greedy_b32": small,
             "config1_single_wav": single,
-            "config5_beam16_lm": lm_line,
+            "config4_beam8_sharded": sharded.get("config4"),
+            "config5_beam16_lm": sharded.get("config5"),
             "f32_exact_path": f32_cmp,
             "kernel_breakdown_ms": {k: round(v[1], 3) for k, v in breakdown.items()},
             "weights_bcast_s": weight_s,

@@ -71,8 +71,20 @@ typedef float ks_f2 __attribute__((ext_vector_type(2)));  // (the k split's 8-by
 #ifndef CASR_LOGITS_NT
 #define CASR_LOGITS_NT 1
 #endif
+// NUMERICS (documented in include/casr.h): with CASR_FAST_PART_EXP = 1 every row's Σexp partial,
+// hence the greedy accum and each beam row's log-sum-exp, differs from the expf form in the last
+// bits (v_exp_f32 is within 1 ulp); tokens are pinned by the oracle tests in both arithmetics
 #ifndef CASR_FAST_PART_EXP
 #define CASR_FAST_PART_EXP 1
+#endif
+
+// The k-split hand-off (dgemm_kernel KS > 1, CASR_OPT_DEC_KSPLIT) orders its agent-scope partial-sum
+// stores before the arrival count with vm_wait<0>() alone: on gfx9-family CDNA (gfx950 here) vmcnt
+// counts stores as well as loads, so the wait retires the sc1 stores at the coherence point before
+// the count is issued.  On gfx10+ stores are counted by vscnt and this would need a release/acquire
+// pair (a device-scope fence measured 33 against 19.5 us per step), so any other target is refused.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "decoder.hip: the k-split hand-off assumes gfx950's vmcnt store counting; build for gfx950 only"
 #endif
 
 __device__ __forceinline__ bool xcd_tile(int NB, int NR, int& nb, int& rb, int L = -1) {
@@ -514,7 +526,7 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
         __hip_atomic_store(p + 1, __builtin_bit_cast(uint64_t, (ks_f2){v[2], v[3]}), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       }
-    vm_wait<0>();  // the sums are stored before the count
+    vm_wait<0>();  // the sums are stored before the count (gfx9 vmcnt counts stores: see the #error above)
     int old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(kscnt + gi, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __shfl(old, 0);

@@ -848,6 +848,9 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
       if (tail == 2 && launch_tail_balanced(km ? X16 : X16 + r0 * Kp, W16, bias, Gin + r0 * N, Mt, N, Kp, ncu, s, km,
                                             (int)r0, M))
         return hipGetLastError();
+      // the row-image tail kernel below cannot read a 16-k-block-major image: a km image whose
+      // balanced tail was not taken is refused, never read as rows
+      if (km) return hipErrorInvalidValue;
       const Order16 ot{NB, NMt, NG};  // XCD grouping of the tail: the same column slices per XCD
       hipLaunchKernelGGL((gemm16_bias_kernel<4, 1>), dim3(ot.blocks()), dim3(256), 0, s, X16 + r0 * Kp, W16, bias,
                          Gin + r0 * N, Mt, N, Kp, ot);

@@ -280,6 +280,14 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            three-launch step; scores within 2e-3, alignments within 1e-5
  *                            (tests/test_gpu_parity.py test_decode_fold_vs_three_launches,
  *                            test_beam_fold_vs_three_launches).  Not used by casr_beam at k = 1.
+ * Two numerics choices are compile-time, not options (both on in the shipped build; the oracle
+ * tests pin the tokens with them, both arithmetics):
+ *   CASR_FAST_PART_EXP       (decoder.hip) the projection epilogue's per-block Σexp(x - max) partials
+ *                            use v_exp_f32 of (x - max) log2(e) instead of libm expf: each row's
+ *                            log-sum-exp, so the greedy accum and every beam score, moves in the
+ *                            last bits (within the 2e-3 score tolerance), and at a near tie of two
+ *                            beam candidates their rank can differ from an expf build's
+ *   CASR_LOGITS_NT           (decoder.hip) beam logits stored with the non-temporal hint: speed only
  * One option exists for tests only:
  *   CASR_OPT_REC_COOP_REFUSE 0 (default): off; n in 1..8: casr_encode treats the cooperative launch
  *                            of encoder layer n - 1 as refused (hipErrorCooperativeLaunchTooLarge,
