@@ -507,6 +507,7 @@ def main():
                                "BASELINE config 5: beam 16 + second-pass LM rescoring (stub LM, host)") +
                               f", {G} utterances sharded over {world} GPU(s), T={T}",
                     "k": kk, "global_batch": G, "batch_per_gpu": len(my_idx), "world_size": world,
+                    "device_batch": min(dec.max_batch, len(my_idx)),
                     "devices": [n for _, n in sorted(dev_names)], "batches": nb,
                     "value": G * nb / dts, "unit": "utt/s", "ms_per_batch": 1000.0 * dts / nb,
                     "rtf": dts / nb / (G * AUDIO_S_PER_UTT), "scaling": "strong",

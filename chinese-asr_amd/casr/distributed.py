@@ -167,60 +167,87 @@ class BeamShardDecoder:
     casr_encode_fbank + casr_beam (model.py:604-987) and, with an LM, the finished-hypothesis
     records to the host and the second pass over them (second_pass_arrays, model.py:749-763;
     the rest keep the device's unfinished fallback / first max, :961-972), exactly as the drop-in
-    Model.eval_one_batch_with_beam does.  enqueue() puts a batch's device work and its copies into
-    pinned host buffers on the stream and returns at once; finish() waits for that batch and runs
-    the host part, so the host part of one batch can overlap the device work of the next (two
-    pinned slots)."""
+    Model.eval_one_batch_with_beam does.
+
+    A shard larger than `max_batch` utterances is decoded as consecutive batches of at most that
+    many (256: the largest batch whose encoder recurrence runs persistent, one workgroup per CU;
+    beyond it the recurrence falls back to per-step launches, casr_recurrence_mode).  Like any
+    batching of the reference's beam search, the batch a hypothesis is decoded in decides when the
+    search stops (model.py:897-901), so the second pass sees the records of its own batch's steps.
+
+    enqueue() puts every batch's device work and its copies into pinned host buffers on the
+    stream and returns at once; finish() waits for one batch at a time and runs its host part, so
+    the host part of one batch overlaps the device work of the next (two pinned slots per batch
+    position)."""
 
     def __init__(self, engine, k, lm_model=None, int2word=None, lm_weight=0.0, length_weight=0.0,
-                 keep_records=False):
+                 keep_records=False, max_batch=256):
         self.engine, self.k = engine, int(k)
-        self.keep_records = keep_records  # finish() keeps the last batch's record arrays (tests)
+        self.keep_records = keep_records  # finish() keeps the last shard's record arrays (tests)
         self.last_records = None
         self.lm_model, self.int2word = lm_model, int2word
         self.lm_weight, self.length_weight = float(lm_weight), float(length_weight)
         self.max_len = engine.cfg.max_len
+        self.max_batch = int(max_batch)
         self._slots = {}
         self._next = 0
         self.stats = {}
 
     def enqueue(self, fbank, frames):
         e = self.engine
-        e.encode_fbank(fbank, frames)
-        r = e.beam(self.k, self.lm_weight, self.length_weight)
-        dev_out = [r["tokens"], r["length"], r["score"], r["steps"]]
-        if self.lm_model is not None:
-            dev_out += list(e.beam_records())
+        n = int(fbank.shape[0])
         slot = self._next & 1
         self._next += 1
-        key = (slot, tuple(tuple(x.shape) for x in dev_out))
-        bufs = self._slots.get(key)
-        if bufs is None:
-            bufs = self._slots[key] = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in dev_out]
-        for h, x in zip(bufs, dev_out):
-            h.copy_(x, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        return bufs, ev
+        pend = []
+        for i, c0 in enumerate(range(0, n, self.max_batch)):
+            c1 = min(n, c0 + self.max_batch)
+            e.encode_fbank(fbank[c0:c1], frames[c0:c1])
+            r = e.beam(self.k, self.lm_weight, self.length_weight)
+            dev_out = [r["tokens"], r["length"], r["score"], r["steps"]]
+            if self.lm_model is not None:
+                dev_out += list(e.beam_records())
+            key = (slot, i, tuple(tuple(x.shape) for x in dev_out))
+            bufs = self._slots.get(key)
+            if bufs is None:
+                bufs = self._slots[key] = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in dev_out]
+            for h, x in zip(bufs, dev_out):
+                h.copy_(x, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            pend.append((bufs, ev))
+        return pend
 
-    def finish(self, pend):
+    def _finish_batch(self, bufs, ev):
         from .results import second_pass_arrays
-        bufs, ev = pend
         ev.synchronize()  # this batch only (the guard bits are the caller's: reading them syncs the stream)
         toks, blen, score, steps = (b.numpy().copy() for b in bufs[:4])
-        self.stats["steps"] = int(steps[0])
+        recs = None
         if self.lm_model is not None:
             rt, rs, rv = (b.numpy() for b in bufs[4:])
             best = second_pass_arrays(rt, rs, rv, self.int2word, self.lm_model, self.lm_weight,
                                       self.length_weight)
-            self.stats["records"] = int(np.count_nonzero(rv))
+            self.stats["records"] = self.stats.get("records", 0) + int(np.count_nonzero(rv))
             if self.keep_records:
-                self.last_records = (rt.copy(), rs.copy(), rv.copy())
+                recs = (rt.copy(), rs.copy(), rv.copy())
             for b, (t, s) in best.items():
                 toks[b, :len(t)] = t
                 blen[b] = len(t)
                 score[b] = s
-        return pack_results(toks, blen, score, self.max_len)
+        return pack_results(toks, blen, score, self.max_len), int(steps[0]), recs
+
+    def finish(self, pend):
+        self.stats["records"] = 0
+        parts, steps, recs = [], [], []
+        for bufs, ev in pend:
+            p, st, rc = self._finish_batch(bufs, ev)
+            parts.append(p)
+            steps.append(st)
+            recs.append(rc)
+        self.stats["steps"] = steps[-1]
+        self.stats["batch_steps"] = steps
+        if self.keep_records and self.lm_model is not None:
+            self.last_records = tuple(np.concatenate([r[i] for r in recs]) for i in range(3))
+        return np.concatenate(parts)
 
 
 def decode_rank(lens, rank, world, load_shard, decoder):

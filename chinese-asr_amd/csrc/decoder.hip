@@ -843,7 +843,7 @@ __device__ __forceinline__ void proj_logits_out(const f32x4 (&acc)[NTN], const f
       continue;
     }
     if (!logits) continue;
-    if (row < R) {
+    if (row < R && !(CASR_DG_DIAG & 256)) {  // (diagnostic bit 256: no logits stores, wrong data)
       float* dst = logits + (size_t)row * V + col;
       if (vec && col + 3 < V) {
 #if CASR_LOGITS_NT

@@ -85,11 +85,12 @@ def test_fused_select_temperature_07(k, B, kpb):
     np.testing.assert_allclose(sc[rows], ref["score"], rtol=0, atol=2e-3)
 
 
-def _tied_weights(cfg, n_tied=400, first=700, lift=30.0):
+def _tied_weights(cfg, n_tied=400, first=700, lift=1000.0):
     """The bench recipe with n_tied vocabulary rows of the projection made identical (row `first`
     copied, the same bias lifted by `lift`): those tokens' logits are equal bit for bit in every
     row (the same products in the same order), and they are the top candidates of every beam row,
-    so more than BS_CAP = 256 candidates sit exactly at the threshold."""
+    so more than BS_CAP = 256 candidates sit exactly at the threshold.  (The lift must exceed the
+    spread of the other logits, tens at the x40 peaking: a +30 lift left other tokens on top.)"""
     enc_sd, dec_sd = synthetic_state_dicts(cfg, peaked=True, eos_bias=0.0)
     W = dec_sd["proj_linear.weight"].copy()
     bias = dec_sd["proj_linear.bias"].copy()
@@ -104,14 +105,16 @@ def _tied_weights(cfg, n_tied=400, first=700, lift=30.0):
 def test_fused_select_heavy_tie_past_bs_cap(k, B, kpb):
     """400 vocabulary entries tied exactly at the top of every row: the threshold candidates
     overflow BS_CAP and the select takes the sorted-list path over the whole row.  Fused and
-    launched bitwise equal; the chosen tokens are the tied block's lowest ids, as the oracle's
-    stable order gives (4 utterances compared with it)."""
+    launched bitwise equal; every decoded token is from the tied block, the hypotheses run all 40
+    steps, and 4 utterances equal the oracle's (its stable order resolves the ties to the lower
+    flat index, as the select's better() does)."""
     cfg = CasrConfig()
     enc_sd, dec_sd = _tied_weights(cfg)
     frames = _frames(B, 33, 20, 60)
     r = _run_fused_vs_launches(cfg, enc_sd, dec_sd, B, k, kpb, frames)
     toks, blen = r["tokens"].numpy(), r["length"].numpy()
-    assert ((toks[:, 0] >= 700) & (toks[:, 0] < 1100)).all()
+    assert (blen == cfg.max_len).all()  # no EOS can outrank the lifted block
+    assert ((toks >= 700) & (toks < 1100)).all()
     rows = [0, B // 3, 2 * B // 3, B - 1]
     feats = [O.features_from_fbank(fbank_for(b, int(frames[b]))) for b in rows]
     ref = O.beam_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd, k)

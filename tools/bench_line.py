@@ -20,10 +20,12 @@ def main(path):
     f32 = d.get("f32_exact_path") or {}
     if f32.get("ms_per_step"):
         parts.append(f"| f32 {f32['ms_per_step']:.3f} ms")
-    for c in ("config3_beam8_b128", "config2_greedy_b32", "config5_beam16_lm", "config1_single_wav"):
+    for c in ("config3_beam8_b128", "config2_greedy_b32", "config4_beam8_sharded", "config5_beam16_lm",
+              "config1_single_wav"):
         x = d.get(c) or {}
-        if x.get("ms_per_step") or x.get("ms_per_call"):
-            parts.append(f"| {c} {x.get('ms_per_step', x.get('ms_per_call')):.3f} ms")
+        ms = x.get("ms_per_step") or x.get("ms_per_batch") or x.get("latency_ms")
+        if ms:
+            parts.append(f"| {c} {ms:.3f} ms" + (f" ({x['value']:.0f} utt/s)" if x.get("value") else ""))
     parts.append(f"| flags {d.get('device_flags_clean')}")
     print(" ".join(parts))
 

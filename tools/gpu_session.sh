@@ -17,6 +17,9 @@
 #                    counter sets in PMC_SETS (';'-separated passes) into $OUT/pmc<PMC_TAG>_<mode>;
 #                    CASR_OPTS=$PMC_OPTS (default REC_COOP=0, the ordinary recurrence launch: DESIGN
 #                    3.2, a cooperative launch ends in SIGSEGV under rocprofv3)
+#   profbeam         rocprofv3 kernel trace + stats of tools/probes/one_step.py at beam 8, B = 256 and 128
+#   probe            python $PROBE once (tools/probes/*.py)
+#   ablibs           tools/probes/ab_libs.sh (LIBS, AB_ARGS, AB_ROUNDS): interleaved library-build A/B
 #   trace            tools/rec_trace.py
 #   prof             rocprofv3 kernel trace + stats of bench.py (greedy only) on the shipped
 #                    cooperative launch; its exit status is recorded (must be the LAST stage)
@@ -65,11 +68,14 @@ for s in $STAGES; do
       timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1
       rc=$?; grep -ciE "counter|name" $OUT/counters.txt; stop_on $rc counters $OUT/counters.txt ;;
     pmc)
-      IFS=';' read -r -a sets <<< "${PMC_SETS:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE;FETCH_SIZE;WRITE_SIZE}"
+      DEFSETS="${PMC_SETS:-SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE;FETCH_SIZE;WRITE_SIZE}"
       for mode in ${PMC_MODES:-greedy beam}; do
+        mv_="PMC_SETS_$mode"  # per-mode counter sets (PMC_SETS_greedy=...), else the common ones
+        IFS=';' read -r -a sets <<< "${!mv_:-$DEFSETS}"
         P=$OUT/pmc${PMC_TAG}_$mode
         mkdir -p $P
-        if [ $mode = beam ]; then export BEAM=8 B=256; else unset BEAM; export B=256; fi
+        if [ $mode = beam ]; then export BEAM=8 B=256; elif [ $mode = beam128 ]; then export BEAM=8 B=128;
+        else unset BEAM; export B=256; fi
         for i in "${!sets[@]}"; do
           CASR_OPTS=${PMC_OPTS:-REC_COOP=0} timeout -s KILL 120 rocprofv3 --pmc ${sets[$i]} --output-format csv -d $P/p$i -o p$i -- \
             python3 tools/probes/one_step.py > $P/p$i.log 2>&1
@@ -77,6 +83,24 @@ for s in $STAGES; do
         done
       done
       unset BEAM B ;;
+    profbeam)
+      # kernel trace + stats of beam 8 at B = 256 (the metric's beam line) and at B = 128 (config 3),
+      # tools/probes/one_step.py, ordinary recurrence launch (a cooperative launch ends in SIGSEGV at
+      # exit under rocprofv3)
+      for bb in 256 128; do
+        BEAM=8 B=$bb STEPS=${PROF_STEPS:-6} CASR_OPTS=REC_COOP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d $OUT/profbeam$bb -o run -- python3 tools/probes/one_step.py > $OUT/profbeam$bb.log 2>&1
+        rc=$?; stop_on $rc "profbeam $bb" $OUT/profbeam$bb.log
+        python tools/prof_by_grid.py $OUT/profbeam$bb/run_kernel_trace.csv 30 > $OUT/prof_by_grid_beam$bb.txt 2>&1
+        head -12 $OUT/prof_by_grid_beam$bb.txt
+      done ;;
+    probe)
+      # PROBE = a python script (tools/probes/...), run once
+      timeout -k 10 ${PROBE_LIMIT:-300} python -u $PROBE > $OUT/probe.log 2>&1
+      rc=$?; tail -20 $OUT/probe.log; stop_on $rc probe $OUT/probe.log ;;
+    ablibs)
+      OUT=$OUT/ablibs timeout -k 10 ${ABLIBS_LIMIT:-600} bash tools/probes/ab_libs.sh > $OUT/ablibs.log 2>&1
+      rc=$?; cat $OUT/ablibs.log | tail -20; stop_on $rc ablibs $OUT/ablibs.log ;;
     trace)
       timeout -k 10 300 python tools/rec_trace.py > $OUT/rec_trace.txt 2>&1
       rc=$?; tail -20 $OUT/rec_trace.txt; stop_on $rc trace $OUT/rec_trace.txt ;;
