@@ -213,6 +213,11 @@ def main():
                     help="MFMA arithmetic of the timed path (casr_set_precision)")
     ap.add_argument("--no-f32-compare", action="store_true",
                     help="skip the side measurement of the exact-f32 MFMA path")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="greedy headline: batches in flight on the GPU (handles / HIP streams, casr.pipeline)")
+    ap.add_argument("--beam-streams", type=int, default=2, help="batches in flight for the metric's beam line")
+    ap.add_argument("--config2-streams", type=int, default=4,
+                    help="BASELINE config 2's pipelined side measurement (its line itself is one batch in flight)")
     ap.add_argument("--graphs", type=int, default=0,
                     help="1: hipGraph replay of the decode loop (casr_set_graphs); default 0: eager launches")
     args = ap.parse_args()
@@ -249,9 +254,13 @@ def main():
         packed = broadcast_packed(packed, dev, expect_floats=packed_floats(cfg))
     torch.cuda.synchronize()
     weight_s = time.perf_counter() - t_w
-    eng = Engine(cfg, packed=packed, device=dev)
-    eng.set_precision(args.precision)
-    eng.set_graphs(2 | (1 if args.graphs else 0))
+    # batches in flight on this GPU (casr.pipeline.StreamPipeline): handle i mod n on stream i mod n;
+    # handle 0 is the serial loop's (n = 1) and runs every instrumented single step
+    from casr.pipeline import StreamPipeline
+    pipe = StreamPipeline(cfg, packed, n=max(1, args.streams, args.beam_streams, args.config2_streams), device=dev)
+    pipe.set_precision(args.precision)
+    pipe.set_graphs(2 | (1 if args.graphs else 0))
+    eng = pipe.engines[0]
     precision = eng.precision()  # effective (f32 if the blob's s16 images are unusable)
 
     B, T = args.batch, args.frames
@@ -259,23 +268,27 @@ def main():
     frames = torch.full((B,), T, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
 
-    # Each step ends with its token ids in host memory: copied into one of two pinned buffers on
-    # the compute stream, without a per-step host sync, so the host's launch work of step i+1 is
-    # not a gap on the GPU between steps (the timed region's closing sync covers every copy).
+    # Each step ends with its token ids in host memory: copied into a ring of pinned buffers on the
+    # step's stream, without a per-step host sync, so the host's launch work of step i+1 is not a
+    # gap on the GPU between steps (the timed region's closing sync covers every copy).  The ring
+    # has two slots per handle, so a slot is only ever written from one stream.
     pin = {}
+    NPIN = 2 * pipe.n
 
     def to_host(t, tag):
         bufs = pin.get((tag, t.shape, t.dtype))
         if bufs is None:
-            bufs = pin[(tag, t.shape, t.dtype)] = [[torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for _ in range(2)], 0]
-        h = bufs[0][bufs[1] & 1]
+            bufs = pin[(tag, t.shape, t.dtype)] = [[torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+                                                    for _ in range(NPIN)], 0]
+        h = bufs[0][bufs[1] % NPIN]
         bufs[1] += 1
         h.copy_(t, non_blocking=True)
         return h
 
-    def step_greedy():
-        eng.encode_fbank(fb, frames)  # features + encoder (casr_encode_fbank)
-        out = eng.greedy()
+    def step_greedy(e=None):
+        e = e or eng
+        e.encode_fbank(fb, frames)  # features + encoder (casr_encode_fbank)
+        out = e.greedy()
         return to_host(out["tokens"], "greedy")
 
     def barrier():
@@ -284,24 +297,34 @@ def main():
 
     flags = {}  # device guard bits read after every timed region (read and clear: all its steps)
 
-    step_ms = {}  # per-step device time (HIP events on the compute stream around each step)
+    step_ms = {}  # per-step device span (HIP events on the step's stream around the step)
 
-    def timed(fn, steps, tag, e=None):
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    def timed(fn, steps, tag, e=None, n=1):
+        """Time exactly `steps` steps fn(engine), bracketed by barrier + synchronize (every
+        stream); with n > 1 consecutive steps go to the pipeline's first n handles in turn, so up
+        to n batches are in flight.  Returns the max over ranks of the wall time."""
+        spans = []
+
+        def one(h):
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn(h)
+            b.record()
+            spans.append((a, b))
+        pipe.reset()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        evs[0].record()
         for i in range(steps):
-            fn()
-            evs[i + 1].record()
+            pipe.submit(one, n)
         torch.cuda.synchronize()
         barrier()
         dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         if dist is not None:
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        flags[tag] = (e or eng).device_flags()
-        step_ms[tag] = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+        flags[tag] = e.device_flags() if e is not None else pipe.device_flags()
+        step_ms[tag] = [a.elapsed_time(b) for a, b in spans]
         return float(dt.item())
 
     def step_stats(tag):
@@ -320,11 +343,15 @@ def main():
     step_greedy()
     breakdown = eng.profile_read()
     dominant = max(breakdown, key=lambda c: breakdown[c][1])
-    # timed region: only the dominant class keeps its event pair per launch
-    eng.profile([dominant])
-    dt = timed(step_greedy, args.steps, "greedy")
-    dom_launches, dom_ms = eng.profile_read()[dominant]
-    eng.profile([])
+    # timed region (args.streams batches in flight): only the dominant class keeps its event pair
+    # per launch, on every handle
+    for _ in range(args.streams):  # every handle of the timed region warm
+        pipe.submit(step_greedy, args.streams)
+    flags["warmup_pipeline"] = pipe.device_flags()
+    pipe.profile([dominant])
+    dt = timed(step_greedy, args.steps, "greedy", n=args.streams)
+    dom_launches, dom_ms = pipe.profile_read()[dominant]
+    pipe.profile([])
 
     Tp = T // 3
     value = B * world * args.steps / dt
@@ -373,24 +400,29 @@ def main():
     avg_launch_s = dom["avg_launch_us"] / 1e6
     traffic = dom.get("traffic")
 
-    def beam_line(Bb, k, steps, tag):
+    def beam_line(Bb, k, steps, tag, n=1):
         fbb = torch.from_numpy(fbank_batch(rank * Bb, Bb, T)).to(dev)
         frb = torch.full((Bb,), T, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
 
-        def step_beam():
-            eng.encode_fbank(fbb, frb)
-            r = eng.beam(k)
+        def step_beam(e=None):
+            e = e or eng
+            e.encode_fbank(fbb, frb)
+            r = e.beam(k)
             return to_host(r["tokens"], tag)
 
-        step_beam()
-        flags[tag + "_warmup"] = eng.device_flags()
-        dtb = timed(step_beam, steps, tag)
+        pipe.reset()
+        for _ in range(n):
+            pipe.submit(step_beam, n)
+        flags[tag + "_warmup"] = pipe.device_flags()
+        dtb = timed(step_beam, steps, tag, n=n)
         # one instrumented beam step after the timed region: per-class milliseconds
         eng.profile(CLASSES)
         step_beam()
         bd = eng.profile_read()
         eng.profile([])
         return {"k": k, "batch_per_gpu": Bb, "value": Bb * world * steps / dtb, "steps": steps,
+                "batches_in_flight": n,
                 "device_ms_per_step": step_stats(tag),
                 "unit": "utt/s", "ms_per_step": 1000.0 * dtb / steps,
                 "rtf": dtb / steps / (Bb * world * AUDIO_S_PER_UTT),
@@ -402,10 +434,11 @@ def main():
     beam = config3 = None
     if not args.no_beam:
         # the metric's beam line: beam 8 at B = 256 per GPU (R = 2048 decode rows)
-        beam = beam_line(args.beam_batch, args.beam, args.beam_steps, "beam")
+        beam = beam_line(args.beam_batch, args.beam, args.beam_steps, "beam", n=args.beam_streams)
         # BASELINE config 3: beam 8 at B = 128 per GPU (config 4 at --gpus 8: 1024 utterances)
         if not args.no_configs:
-            config3 = beam_line(args.config3_batch, args.beam, args.beam_steps, "config3")
+            # (one batch in flight: two measured slower at B = 128, profiles/r06/stream_sweep.log)
+            config3 = beam_line(args.config3_batch, args.beam, args.beam_steps, "config3", n=1)
             config3["config"] = "BASELINE config 3 (config 4 at --gpus 8): beam 8, B=128/GPU, T=800"
 
     # BASELINE config 2: a B = 32 greedy batch (same weights, same step)
@@ -414,13 +447,15 @@ def main():
         Bs = 32
         fbs = torch.from_numpy(fbank_batch(rank * Bs, Bs, T)).to(dev)
         frs = torch.full((Bs,), T, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
 
-        def step_small():
-            eng.encode_fbank(fbs, frs)
-            return to_host(eng.greedy()["tokens"], "small")
+        def step_small(e=None):
+            e = e or eng
+            e.encode_fbank(fbs, frs)
+            return to_host(e.greedy()["tokens"], "small")
 
         step_small()
-        dts = timed(step_small, args.steps, "config2")
+        dts = timed(step_small, args.steps, "config2")  # one batch in flight: the latency
         eng.profile(CLASSES)  # one instrumented step: where a B = 32 batch spends its time
         step_small()
         bds = eng.profile_read()
@@ -428,7 +463,21 @@ def main():
         small = {"config": "BASELINE config 2: greedy, B=32/GPU, T=800", "batch_per_gpu": Bs,
                  "device_ms_per_step": step_stats("config2"),
                  "kernel_breakdown_ms": {c: round(v[1], 3) for c, v in bds.items()},
-                 "value": Bs * world * args.steps / dts, "unit": "utt/s", "ms_per_step": 1000.0 * dts / args.steps}
+                 "value": Bs * world * args.steps / dts, "unit": "utt/s", "ms_per_step": 1000.0 * dts / args.steps,
+                 "batches_in_flight": 1}
+        nc2 = args.config2_streams
+        if nc2 > 1:  # the same B = 32 batches with nc2 in flight (a B = 32 batch fills a quarter of the CUs)
+            pipe.reset()
+            for _ in range(nc2):
+                pipe.submit(step_small, nc2)
+            dtp = timed(step_small, max(args.steps, 2 * nc2), "config2_pipelined", n=nc2)
+            nst = max(args.steps, 2 * nc2)
+            small["pipelined"] = {"batches_in_flight": nc2, "value": Bs * world * nst / dtp, "unit": "utt/s",
+                                  "ms_per_step": 1000.0 * dtp / nst,
+                                  "device_ms_per_step": step_stats("config2_pipelined"),
+                                  "note": "throughput with nc2 B = 32 batches in flight on nc2 handles / streams; "
+                                          "ms_per_step is wall time per batch, device_ms_per_step each batch's own "
+                                          "span (its latency under the overlap)".replace("nc2", str(nc2))}
 
     # BASELINE config 1: one 8 s WAV, greedy, through the drop-in main.parse (main.py:27-65):
     # 16 kHz samples on the host -> log-mel, delta / stack / CMVN -> encoder -> greedy -> text.
@@ -480,8 +529,14 @@ def main():
         else:
             dev_names = [(0, names[0])]
         for tag, kk, lm_on in (("config4", args.beam, False), ("config5", 16, True)):
-            e_sh = eng if not lm_on else Engine(cfg, *synthetic_state_dicts(cfg, peaked=True), device=dev)
-            e_sh.set_precision(args.precision)
+            # each rank's shard in batches of <= 256 with args.beam_streams of them in flight
+            if lm_on:
+                pipe5 = StreamPipeline(cfg, torch.from_numpy(pack_weights(cfg, *synthetic_state_dicts(cfg, peaked=True))).to(dev),
+                                       n=max(1, args.beam_streams), device=dev)
+                pipe5.set_precision(args.precision)
+                e_sh = pipe5
+            else:
+                e_sh = pipe.limited(max(1, args.beam_streams))
             lm = _StubLM() if lm_on else None
             dec = BeamShardDecoder(e_sh, kk, lm, {i: chr(0xE000 + i) for i in range(cfg.vocab)} if lm_on else None,
                                    1.5 if lm_on else 0.0, 1.5 if lm_on else 0.0)
@@ -501,7 +556,7 @@ def main():
                 t_host[0] += time.perf_counter() - t0
                 return r
             dec.finish = timed_finish
-            dts = timed(lambda: [None for _ in decode_sharded(batches(nb), dec, device=gdev)], 1, tag, e=e_sh)
+            dts = timed(lambda h: [None for _ in decode_sharded(batches(nb), dec, device=gdev)], 1, tag, e=e_sh)
             gc.unfreeze()
             line = {"config": ("BASELINE config 4: beam 8" if not lm_on else
                                "BASELINE config 5: beam 16 + second-pass LM rescoring (stub LM, host)") +
@@ -523,6 +578,7 @@ def main():
                             lm="deterministic stub, one call per hypothesis of every utterance with > 1 "
                                "(the reference's call pattern, model.py:755); a KenLM call costs more")
             sharded[tag] = line
+            line["batches_in_flight"] = e_sh.n
             if lm_on:
                 e_sh.close()
 
@@ -531,7 +587,7 @@ def main():
     if precision == "s16x3" and not args.no_f32_compare:
         eng.set_precision("f32")
         step_greedy()
-        dtf = timed(step_greedy, max(2, args.steps // 2), "f32")
+        dtf = timed(step_greedy, max(2, args.steps // 2), "f32", e=eng)  # one batch in flight
         nf = max(2, args.steps // 2)
         f32_cmp = {"value": B * world * nf / dtf, "unit": "utt/s", "ms_per_step": 1000.0 * dtf / nf}
         eng.set_precision(precision)
@@ -596,7 +652,7 @@ def main():
         if cpu:
             rec["speedup_vs_cpu"] = value / cpu["value"]
         print(json.dumps(rec), flush=True)
-    eng.close()  # drain and free the handle now, not from __del__ at interpreter exit
+    pipe.close()  # drain and free the handles now, not from __del__ at interpreter exit
     if dist is not None:
         dist.destroy_process_group()
 

@@ -182,6 +182,8 @@ class BeamShardDecoder:
 
     def __init__(self, engine, k, lm_model=None, int2word=None, lm_weight=0.0, length_weight=0.0,
                  keep_records=False, max_batch=256):
+        # engine: an Engine, or a casr.pipeline.StreamPipeline (or its limited() view), whose
+        # handles then take the shard's batches in turn, several in flight
         self.engine, self.k = engine, int(k)
         self.keep_records = keep_records  # finish() keeps the last shard's record arrays (tests)
         self.last_records = None
@@ -193,28 +195,32 @@ class BeamShardDecoder:
         self._next = 0
         self.stats = {}
 
+    def _batch(self, e, fbank, frames, key):
+        e.encode_fbank(fbank, frames)
+        r = e.beam(self.k, self.lm_weight, self.length_weight)
+        dev_out = [r["tokens"], r["length"], r["score"], r["steps"]]
+        if self.lm_model is not None:
+            dev_out += list(e.beam_records())
+        key = key + (tuple(tuple(x.shape) for x in dev_out),)
+        bufs = self._slots.get(key)
+        if bufs is None:
+            bufs = self._slots[key] = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in dev_out]
+        for h, x in zip(bufs, dev_out):
+            h.copy_(x, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()  # on the batch's stream
+        return bufs, ev
+
     def enqueue(self, fbank, frames):
-        e = self.engine
         n = int(fbank.shape[0])
         slot = self._next & 1
         self._next += 1
+        submit = getattr(self.engine, "submit", None)
         pend = []
         for i, c0 in enumerate(range(0, n, self.max_batch)):
             c1 = min(n, c0 + self.max_batch)
-            e.encode_fbank(fbank[c0:c1], frames[c0:c1])
-            r = e.beam(self.k, self.lm_weight, self.length_weight)
-            dev_out = [r["tokens"], r["length"], r["score"], r["steps"]]
-            if self.lm_model is not None:
-                dev_out += list(e.beam_records())
-            key = (slot, i, tuple(tuple(x.shape) for x in dev_out))
-            bufs = self._slots.get(key)
-            if bufs is None:
-                bufs = self._slots[key] = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in dev_out]
-            for h, x in zip(bufs, dev_out):
-                h.copy_(x, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            pend.append((bufs, ev))
+            fn = (lambda e, c0=c0, c1=c1, i=i: self._batch(e, fbank[c0:c1], frames[c0:c1], (slot, i)))
+            pend.append(submit(fn) if submit else fn(self.engine))
         return pend
 
     def _finish_batch(self, bufs, ev):
