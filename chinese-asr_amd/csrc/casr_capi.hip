@@ -574,8 +574,8 @@ int casr_recurrence_mode(const casr_handle* h, int B) {
 int casr_set_option(casr_handle* h, int option, int value) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
-  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 2, 2, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1, 1, 1, 1, 1};
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 2, 2, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1, 1, 1, 1, 1, 1};
   if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
     return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
   if (value < lo[option] || value > hi[option])
@@ -722,7 +722,8 @@ static int encode_impl(casr_handle* h, const float* feat, const int32_t* lens, i
       HIP_OK(h, launch_input_proj_s16_big(h->x16.as<float>(), (int)rows, kp,
                                           km ? h->wih16km.as<float>() + h->wih16km_off[l] : h->W + h->L.enc_wih16[l],
                                           h->W + h->L.enc_bias[l], h->gin.as<float>(), s, din,
-                                          h->tune[CASR_OPT_GEMM16_PERSIST], h->tune[CASR_OPT_GEMM16_TAIL], km));
+                                          h->tune[CASR_OPT_GEMM16_PERSIST], h->tune[CASR_OPT_GEMM16_TAIL], km,
+                                          h->tune[CASR_OPT_GEMM16_LEAN]));
     } else {
       HIP_OK(h, launch_input_proj(x, (int)rows, din, h->W + h->L.enc_wih[l], h->W + h->L.enc_bias[l],
                                   h->gin.as<float>(), s));

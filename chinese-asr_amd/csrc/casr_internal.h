@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1, 1};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1, 1, 0};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -247,7 +247,8 @@ inline bool x16_km(const Tuning& t) {
 // (multiple of 64) k per row (km: both 16-k-block major, X16 with M rows).  K: the real input width
 // (the images are zero from K to Kp); 0 = Kp.  persist / tail: CASR_OPT_GEMM16_PERSIST / _TAIL
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                     float* Gin, hipStream_t s, int K, int persist, int tail, int km = 0);
+                                     float* Gin, hipStream_t s, int K, int persist, int tail, int km = 0,
+                                     int lean = 0);
 // a row-image weight matrix [R][Kp] -> its 16-k-block-major image (bind time)
 hipError_t launch_relayout_km16(const float* rowimg, int R, int Kp, float* km, hipStream_t s);
 hipError_t launch_split_rows(const float* X, int ldx, int M, int K, int Kp, uint16_t* out, int32_t* err,

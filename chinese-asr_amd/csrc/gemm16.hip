@@ -639,6 +639,219 @@ __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restri
 }
 
 
+// ---- lean ping-pong form (round 6, CASR_OPT_GEMM16_LEAN = 1, 16-k-block-major images, nk >= 8).
+// gemm16_pp_kernel<…, KM = true> with the LOAD sections' scalar work cut; the same fragments, MFMAs,
+// DMA bytes, ring slots and barriers in the same order, so the outputs are bitwise equal.  The round-6
+// PMC passes (profiles/r06/gemm16_diag/) put the stage interval in the LOAD sections, not the LDS
+// array (19 % busy, no bank conflicts, LDS-issue stalls 4 % of wave cycles): each wave issued ~65
+// scalar instructions per 16-deep stage (SQ_INSTS_SALU, 3.2 per MFMA) -- 64-bit stage addresses
+// rebuilt with s_mul, the runtime vmcnt ladder of pp_vm_wait (compares and branches, twice per stage)
+// and the count it selects.  Here:
+//   * the DMA sources are running pointers (stage j + 3 of the tile, then the next tile's stages),
+//     advanced by one 32-bit byte stride per stage;
+//   * the stages whose younger VMEM count is fixed (2 <= j < nk - 3: the 8 DMA instructions of
+//     stages j + 2 and j + 3, no bias, no epilogue stores) wait with a constant vmcnt(8);
+//   * the wave index goes through readfirstlane, so the group branches are scalar.
+CASR_DEV void lds_dma16_u(uint32_t voff, const float* sbase, uint32_t lds_byte) {
+  // lds_dma16_s with the base made visibly uniform: the running pointers are carried through a lambda,
+  // where hipcc's divergence analysis loses them (they are uniform: tile indices and strides)
+  const uint64_t u = (uint64_t)(uintptr_t)sbase;
+  const float* sb = (const float*)(uintptr_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32)) << 32) |
+                                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u));
+  lds_dma16_s(voff, sb, lds_byte);
+}
+
+__global__ __launch_bounds__(512, 2) void gemm16_pp_lean_kernel(const float* __restrict__ A16, const float* __restrict__ W16,
+                                                              const float* __restrict__ bias, float* __restrict__ Cout,
+                                                              int M, int N, Order16 order, int total, int nk, int Mimg) {
+  __shared__ __attribute__((aligned(16))) float lds[PP_LDS];
+  constexpr int NT = 2;  // 32-column MFMA tiles per wave (wave tile 128 x 64)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3, grp = wave >> 2;
+  const int r32 = lane & 31, hsel = lane >> 5;
+  const int G = gridDim.x;
+  float* const bias_lds = lds + PP_NBUF * PP_STAGE;
+  auto next_tile = [&](int L, int& n, int& m) {
+    while (L < total && !order.tile(L, n, m)) L += G;
+    return L;
+  };
+  const uint32_t lds_u32 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds;
+  uint32_t vw[2];
+  int coff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 32 + i * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+    coff[i] = 4 * c;
+    vw[i] = (uint32_t)(row * 16 + coff[i]) * 4u;
+  }
+  auto a_offsets = [&](int m, uint32_t (&va)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wave * 32 + i * 16 + (lane >> 2);
+      va[i] = (uint32_t)(min(row, M - 1 - m * G16_M) * 16 + coff[i]) * 4u;
+    }
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const uint32_t a_stb = (uint32_t)Mimg * 64u, w_stb = (uint32_t)N * 64u;  // bytes per 16-k block
+  auto adv = [](const float*& p, uint32_t b) { p = (const float*)((const char*)p + b); };
+  // one stage's DMA into ring buffer b from (pa, pw): this wave's 32 A rows and 32 W rows, plus the
+  // tile's bias with its stage 0 (every wave copies the same 1 KB into the slot)
+  auto dma = [&](int b, const float* sa, const float* sw, const uint32_t (&va)[2], bool with_bias, int nb, int tp) {
+    const uint32_t l0 = lds_u32 + (uint32_t)(b * PP_STAGE + wave * 32 * PP_ROWF) * 4u;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      lds_dma16_u(va[i], sa, l0 + i * 16 * PP_ROWF * 4u);
+      lds_dma16_u(vw[i], sw, l0 + (PP_OP + i * 16 * PP_ROWF) * 4u);
+    }
+    if (with_bias)
+      lds_dma16_u((uint32_t)min(lane * 16, (N - nb * G16_N - 4) * 4), bias + nb * G16_N,
+                  lds_u32 + (uint32_t)(PP_NBUF * PP_STAGE + tp * G16_N) * 4u);
+  };
+
+  int n, m;
+  int L = next_tile(blockIdx.x, n, m);
+  if (L >= total) return;
+  int n2 = n, m2 = m;
+  int L2 = next_tile(L + G, n2, m2);
+  int gb = 0, tpar = 0;
+  uint32_t va[2], va2[2];
+  a_offsets(m, va);
+  a_offsets(m2, va2);
+  const float* pa = A16 + (size_t)m * G16_M * 16;  // the next stage to DMA
+  const float* pw = W16 + (size_t)n * G16_N * 16;
+  for (int s = 0; s < 3; ++s) {  // prologue: stages 0..2 of the first tile (nk >= 8)
+    dma(s, pa, pw, va, s == 0, n, 0);
+    adv(pa, a_stb);
+    adv(pw, w_stb);
+  }
+  pp_vm_wait(8);  // stage 0 (and its bias) landed: younger = stages 1 and 2
+  barrier();
+  bool after_epi = false;
+  const _Float16 two11 = (_Float16)2048.0f;
+  f32x16 acc[4][NT];
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][t][e] = 0.f;
+    auto ex = [&](int s) { return s < nk || L2 < total; };
+    auto ops = [&](int s) { return ex(s) ? 4 + (s == nk ? 1 : 0) : 0; };
+    if (grp == 1) barrier();  // the stagger: group 1 runs one barrier behind group 0
+    auto stage = [&](int j, auto FIXED) {
+      constexpr int fixed = decltype(FIXED)::value;
+      const float* buf = lds + ((gb + j) & 3) * PP_STAGE;
+      // ---- LOAD_j: fragments of stage j, DMA of stage j + 3
+      f16x8 wh[NT], wl[NT], ah[4], al[4];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int row = wn * 64 + t * 32 + r32, sw = (row >> 2) & 3;
+        wh[t] = *reinterpret_cast<const f16x8*>(buf + PP_OP + row * PP_ROWF + ((hsel ^ sw) << 2));
+        wl[t] = *reinterpret_cast<const f16x8*>(buf + PP_OP + row * PP_ROWF + (((2 + hsel) ^ sw) << 2));
+      }
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm) {
+        const int row = wm * 128 + tm * 32 + r32, sw = (row >> 2) & 3;
+        ah[tm] = *reinterpret_cast<const f16x8*>(buf + row * PP_ROWF + ((hsel ^ sw) << 2));
+        al[tm] = *reinterpret_cast<const f16x8*>(buf + row * PP_ROWF + (((2 + hsel) ^ sw) << 2));
+      }
+      const int s3 = j + 3;
+      if (fixed >= 0 || ex(s3)) {
+        if (fixed < 0 && s3 == nk) {  // the next tile's stage 0 (and its bias)
+          pa = A16 + (size_t)m2 * G16_M * 16;
+          pw = W16 + (size_t)n2 * G16_N * 16;
+        }
+        const bool nxt = fixed < 0 && s3 >= nk;
+        dma((gb + s3) & 3, pa, pw, nxt ? va2 : va, fixed < 0 && s3 == nk, n2, tpar ^ 1);
+        adv(pa, a_stb);
+        adv(pw, w_stb);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      f16x8 w1[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) w1[t] = wh[t] * two11;
+      // VMEM operations issued after this wave's DMA of stage j + 1: stages j + 2, j + 3 and, while
+      // stages 1 and 2 of a tile wait, the previous tile's 32 epilogue stores
+      auto vwait = [&] {
+        if constexpr (fixed >= 0) g16_vm_wait<fixed>();
+        else pp_vm_wait(ops(j + 2) + ops(j + 3) + (after_epi && j < 2 ? PP_EPI_STORES : 0));
+      };
+      if (grp == 1 && j + 1 < nk) vwait();
+      barrier();
+      // ---- MFMA_j
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], w1[t], acc[tm][t], 0, 0, 0);
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], wl[t], acc[tm][t], 0, 0, 0);
+          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[tm], wh[t], acc[tm][t], 0, 0, 0);
+        }
+      __builtin_amdgcn_s_setprio(0);
+      if (grp == 0 && j + 1 < nk) vwait();
+      barrier();
+    };
+    using Dyn = std::integral_constant<int, -1>;
+    for (int j = 0; j < 2; ++j) stage(j, Dyn{});
+    for (int j = 2; j < nk - 3; ++j) stage(j, std::integral_constant<int, 8>{});
+    for (int j = nk - 3; j < nk; ++j) stage(j, Dyn{});
+    if (grp == 0) barrier();  // realign the groups: every wave has passed every read of this tile
+    // ---- epilogue (gemm16_pp_kernel's): per wave, 8 rounds of 16 rows x 64 columns through a
+    // private 4 KB slab
+    {
+      float* slab = lds + ((gb + nk - 1) & 3) * PP_STAGE + wave * 16 * 64;
+      const int c4 = lane & 15, rq = lane >> 4;
+      const float4 b4 = *reinterpret_cast<const float4*>(bias_lds + tpar * G16_N + wn * 64 + c4 * 4);
+      const int m0 = m * G16_M;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          Cout + (size_t)m0 * N, 0, (int)((size_t)min(G16_M, M - m0) * N * 4), 0x00020000);
+      const int cbase = n * G16_N + wn * 64 + c4 * 4;
+#pragma unroll
+      for (int tm = 0; tm < 4; ++tm)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int e = 8 * hh; e < 8 * hh + 8; ++e)
+              slab[((e & 3) + 8 * ((e >> 2) & 1) + 4 * hsel) * 64 + t * 32 + r32] = acc[tm][t][e] * S16_LO_INV;
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = rq + 4 * i;
+            const float4 v = *reinterpret_cast<const float4*>(slab + row * 64 + c4 * 4);
+            const int lr = wm * 128 + tm * 32 + 16 * hh + row;  // row within the tile
+            const float4 o = make_float4(v.x + b4.x, v.y + b4.y, v.z + b4.z, v.w + b4.w);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, (lr * N + cbase) * 4, 0,
+                                                   CASR_GIN_NT ? 2 : 0);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    }
+    if (L2 >= total) break;
+    // the next tile's stage 0 (+ bias) landed: younger = its stages 1, 2 and the 32 stores
+    pp_vm_wait(ops(nk + 1) + ops(nk + 2) + PP_EPI_STORES);
+    barrier();  // ... visible to every wave; every wave is done with its epilogue slab
+    gb = (gb + nk) & 3;
+    L = L2;
+    n = n2;
+    m = m2;
+    tpar ^= 1;
+    after_epi = true;
+    L2 = next_tile(L + G, n2, m2);
+    va[0] = va2[0];
+    va[1] = va2[1];
+    a_offsets(m2, va2);
+  }
+}
+
+
 // ---- balanced tail (round 5, CASR_OPT_GEMM16_TAIL = 2, default): the rows after the persistent
 // kernel's whole rounds as (32 RT)-row x 128-column tiles, RT picked so that they fill the CUs in one
 // round (B = 256: 2,560 rows = 16 row blocks of 160 rows x 16 column blocks = 256 tiles; TAIL = 1 ran
@@ -795,7 +1008,7 @@ static bool launch_tail_balanced(const float* A16, const float* W16, const float
 }  // namespace
 
 hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const float* W16, const float* bias,
-                                     float* Gin, hipStream_t s, int K, int persist, int tail, int km) {
+                                     float* Gin, hipStream_t s, int K, int persist, int tail, int km, int lean) {
   const int N = 8 * H;
   if (km && (persist != 2 || tail == 1)) return hipErrorInvalidValue;  // the forms that read 16-k-major images
   if (Kp % (2 * G16_K) != 0 || M <= 0 || N % G16_N != 0) return hipErrorInvalidValue;
@@ -832,7 +1045,10 @@ hipError_t launch_input_proj_s16_big(const float* X16, int M, int Kp, const floa
     const int Mm = std::min(M, NMm * G16_M);
     if (persist == 2) {  // ping-pong form: 16-deep stages
       const int nk16 = (K > 0 && K <= Kp ? K + 15 : Kp) / 16;
-      if (km)
+      if (km && lean && nk16 >= 8)
+        hipLaunchKernelGGL(gemm16_pp_lean_kernel, dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias, Gin, Mm, N,
+                           om, total, nk16, M);
+      else if (km)
         hipLaunchKernelGGL((gemm16_pp_kernel<0, 1, 0, 0, true>), dim3(std::min(total, ncu)), dim3(512), 0, s, X16, W16, bias,
                            Gin, Mm, N, Kp, om, total, nk16, M);
       else

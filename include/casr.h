@@ -251,6 +251,10 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            cache lines (default, round 5; in effect with GEMM16_PERSIST = 2,
  *                            GEMM16_TAIL != 1 and KEYS_ROWS = 1, the forms that read it); 0: row
  *                            images.  The same words in another order: the same bits
+ *   CASR_OPT_GEMM16_LEAN     1: the ping-pong input projection (GEMM16_PERSIST = 2 on 16-k-major
+ *                            images) advances its DMA sources by a stride per stage and waits on
+ *                            constant vmcnt counts in its steady state (round 6); 0: 64-bit stage
+ *                            addresses and the runtime wait ladder.  The same MFMAs in the same order
  * Three options select numerics variants instead (the same token ids, floating-point results within
  * the stated tolerances, not bit for bit; tests/test_gpu_parity.py compares each pair):
  *   CASR_OPT_DEC_KSPLIT      1: the greedy folded GEMM at R <= 32 decode rows (BASELINE config 2)
@@ -319,7 +323,8 @@ enum {
   CASR_OPT_KEYS_ROWS = 14,
   CASR_OPT_X16_KM = 15,
   CASR_OPT_DEC_KSPLIT = 16,
-  CASR_OPT_COUNT = 17
+  CASR_OPT_GEMM16_LEAN = 17,
+  CASR_OPT_COUNT = 18
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

@@ -95,8 +95,11 @@ for s in $STAGES; do
         head -12 $OUT/prof_by_grid_beam$bb.txt
       done ;;
     probe)
-      # PROBE = a python script (tools/probes/...), run once
-      timeout -k 10 ${PROBE_LIMIT:-300} python -u $PROBE > $OUT/probe.log 2>&1
+      # PROBE = a python script (tools/probes/...) or a probe binary built in the container, run once
+      case $PROBE in
+        *.py) timeout -k 10 ${PROBE_LIMIT:-300} python -u $PROBE > $OUT/probe.log 2>&1 ;;
+        *) (cd $(dirname $PROBE) && timeout -k 10 ${PROBE_LIMIT:-300} ./$(basename $PROBE) $PROBE_ARGS) > $OUT/probe.log 2>&1 ;;
+      esac
       rc=$?; tail -20 $OUT/probe.log; stop_on $rc probe $OUT/probe.log ;;
     ablibs)
       OUT=$OUT/ablibs timeout -k 10 ${ABLIBS_LIMIT:-600} bash tools/probes/ab_libs.sh > $OUT/ablibs.log 2>&1
