@@ -207,6 +207,8 @@ def main():
                          "config 5 (beam 16 + LM) side lines")
     ap.add_argument("--sharded-batch", type=int, default=1024,
                     help="global batch of the BASELINE config 4 / 5 lines (partitioned over the ranks)")
+    ap.add_argument("--rescore-workers", type=int, default=6,
+                    help="host worker processes per rank for config 5's second-pass LM calls (0: in-process)")
     ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--cpu-beam-sample", type=int, default=64)
     ap.add_argument("--precision", default="s16x3", choices=["s16x3", "f32"],
@@ -224,6 +226,13 @@ def main():
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(relaunch(args.gpus))
+    # config 5's host second pass on worker processes (casr.rescore): started here, before this
+    # process initialises the GPU (a worker is a fresh interpreter; none of them touches the GPU)
+    rescorer = None
+    if not args.no_configs and args.sharded_batch > 0 and args.rescore_workers > 0:
+        from casr.rescore import ParallelRescorer
+        rescorer = ParallelRescorer(_StubLM, {i: chr(0xE000 + i) for i in range(5004)}, 5004,
+                                    workers=args.rescore_workers)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)", file=sys.stderr)
@@ -343,15 +352,26 @@ def main():
     step_greedy()
     breakdown = eng.profile_read()
     dominant = max(breakdown, key=lambda c: breakdown[c][1])
-    # timed region (args.streams batches in flight): only the dominant class keeps its event pair
-    # per launch, on every handle
-    for _ in range(args.streams):  # every handle of the timed region warm
-        pipe.submit(step_greedy, args.streams)
-    flags["warmup_pipeline"] = pipe.device_flags()
+    # Two timed regions of the same steps.  (1) Serial, one batch in flight: the dominant class keeps
+    # its event pair per launch, so `roofline` is the kernel's own launch duration (as rocprof sees it
+    # in a serial run).  (2) args.streams batches in flight (casr.pipeline): the line's `value`, the
+    # whole-job throughput; a launch there shares the chip with the other batch's kernels, so its span
+    # is longer (reported as roofline.pipelined_avg_launch_us) while the chip does more work per second.
     pipe.profile([dominant])
-    dt = timed(step_greedy, args.steps, "greedy", n=args.streams)
+    dt_serial = timed(step_greedy, args.steps, "greedy_serial", n=1)
     dom_launches, dom_ms = pipe.profile_read()[dominant]
     pipe.profile([])
+    pl_dom = None
+    if args.streams > 1:
+        for _ in range(args.streams):  # every handle of the timed region warm
+            pipe.submit(step_greedy, args.streams)
+        flags["warmup_pipeline"] = pipe.device_flags()
+        pipe.profile([dominant])
+        dt = timed(step_greedy, args.steps, "greedy", n=args.streams)
+        pl_dom = pipe.profile_read()[dominant]
+        pipe.profile([])
+    else:
+        dt = dt_serial
 
     Tp = T // 3
     value = B * world * args.steps / dt
@@ -394,6 +414,7 @@ def main():
         return bd.get("dec_lstm", (0, 0.0))[0] == 1
     fold = folded(breakdown)
     dom = roof(dominant, dom_launches, dom_ms, args.steps, B, B, fold=fold)
+    pl_roof = roof(dominant, pl_dom[0], pl_dom[1], args.steps, B, B, fold=fold) if pl_dom else None
     # every class of the instrumented step (one step: launches and ms of that step)
     kernels = {c: roof(c, n, ms, 1, B, B, fold=fold) for c, (n, ms) in breakdown.items()}
     achieved, peak, unit, bound = dom["achieved"], dom["peak"], dom["unit"], dom["bound"]
@@ -539,7 +560,8 @@ def main():
                 e_sh = pipe.limited(max(1, args.beam_streams))
             lm = _StubLM() if lm_on else None
             dec = BeamShardDecoder(e_sh, kk, lm, {i: chr(0xE000 + i) for i in range(cfg.vocab)} if lm_on else None,
-                                   1.5 if lm_on else 0.0, 1.5 if lm_on else 0.0)
+                                   1.5 if lm_on else 0.0, 1.5 if lm_on else 0.0,
+                                   rescorer=rescorer if lm_on else None)
             batches = lambda n: [(lens_g, lambda idx: (fb_sh, fr_sh))] * n
             for out in decode_sharded(batches(2), dec, device=gdev):
                 pass
@@ -576,7 +598,8 @@ def main():
                 line.update(records_per_batch_rank0=dec.stats.get("records"),
                             weights="synthetic recipe with the EOS bias (hypotheses finish before step 40)",
                             lm="deterministic stub, one call per hypothesis of every utterance with > 1 "
-                               "(the reference's call pattern, model.py:755); a KenLM call costs more")
+                               "(the reference's call pattern, model.py:755); a KenLM call costs more",
+                            rescore_workers=(rescorer.workers if rescorer is not None else 0))
             sharded[tag] = line
             line["batches_in_flight"] = e_sh.n
             if lm_on:
@@ -614,6 +637,11 @@ def main():
                                    f"encoder + 40-step attention decode, ids to host",
                        "global_batch": B * world, "seq_len": T, "parallelism": f"dp{world}"},
             "rtf": dt / args.steps / (B * world * AUDIO_S_PER_UTT),
+            "batches_in_flight": args.streams,
+            "greedy_serial": {"value": B * world * args.steps / dt_serial, "unit": "utt/s",
+                              "ms_per_step": 1000.0 * dt_serial / args.steps,
+                              "device_ms_per_step": step_stats("greedy_serial"),
+                              "note": "the same steps with one batch in flight (the round-5 headline's loop)"},
             "device_ms_per_step": step_stats("greedy"),
             "device_ms_note": "per timed step, HIP events on the compute stream around each step (device "
                               "time incl. any launch gaps; SURVEY 8d: median of the steps)",
@@ -627,6 +655,10 @@ def main():
                          "traffic_unit": "bytes per launch (PMC 2 x FETCH_SIZE + WRITE_SIZE)",
                          "algorithmic_bytes": kernel_bytes(dominant, B, Tp, B, cfg.vocab, fold, precision == "s16x3"),
                          "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s,
+                         "timed_region": "serial pass (one batch in flight) of the same greedy steps; the headline "
+                                         "value is the pass with `batches_in_flight` batches in flight",
+                         "pipelined_avg_launch_us": pl_roof["avg_launch_us"] if pl_roof else None,
+                         "pipelined_frac": pl_roof["frac"] if pl_roof else None,
                          "launch": LAUNCH_UNIT.get(dominant, "one kernel launch"),
                          "peak_basis": ("f16 MFMA dense peak / 3 (s16x3 f32-equivalent)" if bound == "mfma" and
                                         precision == "s16x3" else "spec peak of the bound"),
@@ -653,6 +685,8 @@ def main():
             rec["speedup_vs_cpu"] = value / cpu["value"]
         print(json.dumps(rec), flush=True)
     pipe.close()  # drain and free the handles now, not from __del__ at interpreter exit
+    if rescorer is not None:
+        rescorer.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -181,7 +181,7 @@ class BeamShardDecoder:
     position)."""
 
     def __init__(self, engine, k, lm_model=None, int2word=None, lm_weight=0.0, length_weight=0.0,
-                 keep_records=False, max_batch=256):
+                 keep_records=False, max_batch=256, rescorer=None):
         # engine: an Engine, or a casr.pipeline.StreamPipeline (or its limited() view), whose
         # handles then take the shard's batches in turn, several in flight
         self.engine, self.k = engine, int(k)
@@ -191,6 +191,7 @@ class BeamShardDecoder:
         self.lm_weight, self.length_weight = float(lm_weight), float(length_weight)
         self.max_len = engine.cfg.max_len
         self.max_batch = int(max_batch)
+        self.rescorer = rescorer  # casr.rescore.ParallelRescorer: the LM calls on host worker processes
         self._slots = {}
         self._next = 0
         self.stats = {}
@@ -230,8 +231,11 @@ class BeamShardDecoder:
         recs = None
         if self.lm_model is not None:
             rt, rs, rv = (b.numpy() for b in bufs[4:])
-            best = second_pass_arrays(rt, rs, rv, self.int2word, self.lm_model, self.lm_weight,
-                                      self.length_weight)
+            if self.rescorer is not None:  # the same choice, LM calls spread over worker processes
+                best = self.rescorer.select(rt, rs, rv, self.lm_weight, self.length_weight)
+            else:
+                best = second_pass_arrays(rt, rs, rv, self.int2word, self.lm_model, self.lm_weight,
+                                          self.length_weight)
             self.stats["records"] = self.stats.get("records", 0) + int(np.count_nonzero(rv))
             if self.keep_records:
                 recs = (rt.copy(), rs.copy(), rv.copy())

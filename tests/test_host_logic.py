@@ -88,6 +88,28 @@ def test_second_pass_arrays_equals_record_lists():
                 second_pass_arrays(rt, rsc, rv, partial, lm, 1.5, 1.5)
 
 
+def test_parallel_rescorer_equals_second_pass_arrays():
+    """casr.rescore.ParallelRescorer (config 5's host second pass over worker processes) returns the
+    second_pass_arrays result exactly -- the same record per utterance, the same (tokens, logp) --
+    on random records, with records split over several worker tasks (chunk smaller than the record
+    count), and with no records."""
+    from casr.results import second_pass_arrays
+    from casr.rescore import ParallelRescorer
+    i2w = pua_int2word(5004)
+    pr = ParallelRescorer(StubLM, i2w, 5004, workers=2, chunk=37)
+    try:
+        rs_ = np.random.RandomState(5)
+        for B, L, k, p in ((24, 40, 16, 0.06), (8, 12, 4, 0.3), (4, 6, 2, 0.0)):
+            rv = (rs_.rand(B, L, k) < p).astype(np.uint8)
+            rt = np.full((B, L, k, L), -1, np.int32)
+            for b, l, c in zip(*np.nonzero(rv)):
+                rt[b, l, c, :l] = rs_.randint(0, 5004, size=l)
+            rsc = rs_.randn(B, L, k).astype(np.float32)
+            assert pr.select(rt, rsc, rv, 1.5, 1.5) == second_pass_arrays(rt, rsc, rv, i2w, StubLM(), 1.5, 1.5)
+    finally:
+        pr.close()
+
+
 def test_wer():
     assert edit_distance("abc", "abc") == 0
     assert edit_distance("", "abc") == 3

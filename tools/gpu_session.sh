@@ -109,7 +109,7 @@ for s in $STAGES; do
       rc=$?; tail -20 $OUT/rec_trace.txt; stop_on $rc trace $OUT/rec_trace.txt ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-        python3 bench.py --steps 20 --warmup 2 --no-beam --no-configs --no-f32-compare --no-cpu-baseline \
+        python3 bench.py --steps 20 --warmup 2 --streams 1 --no-beam --no-configs --no-f32-compare --no-cpu-baseline \
         > $OUT/prof_bench.json 2> $OUT/prof.err
       echo "rocprofv3 kernel trace of the default (cooperative) launch: exit status $?" | tee $OUT/prof_rc.txt
       python tools/prof_by_grid.py $OUT/prof/run_kernel_trace.csv 30 > $OUT/prof_by_grid.txt 2>&1
