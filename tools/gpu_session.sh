@@ -87,8 +87,8 @@ for s in $STAGES; do
       # kernel trace + stats of beam 8 at B = 256 (the metric's beam line) and at B = 128 (config 3),
       # tools/probes/one_step.py, ordinary recurrence launch (a cooperative launch ends in SIGSEGV at
       # exit under rocprofv3)
-      for bb in 256 128; do
-        BEAM=8 B=$bb STEPS=${PROF_STEPS:-6} CASR_OPTS=REC_COOP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+      for bb in ${PROF_BATCHES:-256 128}; do
+        BEAM=${PROF_BEAM:-8} B=$bb STEPS=${PROF_STEPS:-6} CASR_OPTS=REC_COOP=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats \
           --output-format csv -d $OUT/profbeam$bb -o run -- python3 tools/probes/one_step.py > $OUT/profbeam$bb.log 2>&1
         rc=$?; stop_on $rc "profbeam $bb" $OUT/profbeam$bb.log
         python tools/prof_by_grid.py $OUT/profbeam$bb/run_kernel_trace.csv 30 > $OUT/prof_by_grid_beam$bb.txt 2>&1
