@@ -36,7 +36,8 @@ PRECISIONS = {"f32": 0, "s16x3": 1}
 OPTIONS = {"FUSE_SELECT": 0, "REC_LAYOUT": 1, "REC_STORE_PLAIN": 2, "REC_SLEEP": 3, "REC_POLL_GAP": 4,
            "REC_COOP": 5, "GEMM16_PERSIST": 6, "GEMM16_TAIL": 7, "ATTN_KPB": 8, "ATTN_DIRECT": 9,
            "DEC_FOLD": 10, "REC_COOP_REFUSE": 11, "DIAG_COLD": 12,
-           "LOGMEL_Q16": 13, "KEYS_ROWS": 14, "X16_KM": 15, "DEC_KSPLIT": 16, "GEMM16_LEAN": 17}
+           "LOGMEL_Q16": 13, "KEYS_ROWS": 14, "X16_KM": 15, "DEC_KSPLIT": 16, "GEMM16_LEAN": 17,
+           "ATTN_SPLIT": 18}
 
 # kernel classes of casr_profile_enable / casr_profile_read (include/casr.h)
 KERNEL_CLASSES = ["features", "input_proj", "rec_step", "keys", "dec_lstm", "attention", "proj", "select"]

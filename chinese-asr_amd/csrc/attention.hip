@@ -26,6 +26,12 @@
 #define CASR_AT_DIAG 0
 #endif
 
+// the split attention's hand-off (TSPLIT) orders its agent-scope stores before the arrival count
+// with vmcnt(0) alone, as decoder.hip's k split: gfx9-family only
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "attention.hip: the split hand-off assumes gfx950's vmcnt store counting; build for gfx950 only"
+#endif
+
 namespace casr {
 
 constexpr int AT_THREADS = 512;
@@ -37,11 +43,15 @@ constexpr int AT_APAD = A + AT_CH;  // q / v rows in LDS, zero-padded so a batch
 
 __host__ __device__ constexpr int attn_tq(int Tp) { return (Tp + 3) & ~3; }
 
-template <int KPB>
+template <int KPB, int MAXG = AT_MAXG>
 __host__ __device__ constexpr int attn_scratch_floats(int Tq) {
-  // score partials [AT_MAXG][KPB][Tq] | context partials [4][KPB][C]
-  return AT_MAXG * KPB * Tq > 4 * KPB * C ? AT_MAXG * KPB * Tq : 4 * KPB * C;
+  // score partials [MAXG][KPB][Tq] | context partials [4][KPB][C]
+  return MAXG * KPB * Tq > 4 * KPB * C ? MAXG * KPB * Tq : 4 * KPB * C;
 }
+// (round 6) the split folded greedy attention (attention_kernel<1, 1, true>): a block takes Tq / S
+// steps, so its score phase can use up to 32 a-groups of 4 keys rows (the unsplit form's 8 groups of
+// 16 rows would leave most of the block's threads idle on a short range)
+constexpr int AT_MAXG_SPLIT = 32;
 
 // the folded step's cell phase (CELL): h [HD] | query slices [AT_QS][A]
 constexpr int AT_QS = AT_THREADS / (A / 4);  // 16 unit slices of HD / AT_QS = 32 units
@@ -51,9 +61,10 @@ static_assert(AT_QS * A >= 4 * HD, "the token's gate-table row fits the query sl
 // LDS: qs, eqs [AT_APAD][KPB] | vs, v2s [A] | (AT_MAXG unused) | scratch | es [Tq][KPB] | (CELL: h,
 // query slices) | value rows
 // (CELL 2, the beam cell phase, keeps its h rows and query slices in the score scratch instead)
-template <int KPB, int CELL = 0>
+template <int KPB, int CELL = 0, bool TSPLIT = false>
 __host__ __device__ constexpr size_t attn_smem_floats(int Tp) {
-  return (size_t)2 * KPB * AT_APAD + 2 * A + AT_MAXG + attn_scratch_floats<KPB>(attn_tq(Tp)) + KPB * attn_tq(Tp) +
+  return (size_t)2 * KPB * AT_APAD + 2 * A + AT_MAXG +
+         attn_scratch_floats<KPB, TSPLIT ? AT_MAXG_SPLIT : AT_MAXG>(attn_tq(Tp)) + KPB * attn_tq(Tp) +
          (CELL == 1 ? AT_CELL_FLOATS : 0);
 }
 
@@ -111,7 +122,14 @@ __device__ uint32_t* g_at_trace = nullptr;
 // from the beam select; gates_prev and c are read at the predecessor row.  CELL 3, beam with one
 // block per utterance (KPB = k = 4 or 8): the block first runs the beam select of step l - 1 for
 // its utterance (beam_select.h) and takes the tokens and predecessor rows from it.
-template <int KPB, int CELL = 0>
+// TSPLIT (round 6, CELL 1 only, CASR_OPT_ATTN_SPLIT): the utterance's time steps are split over
+// cell.split blocks (blockIdx.y = the split, cell.tc steps each, a multiple of 4).  Every block runs
+// the select, the cell and the query (identical values; only split 0 writes the bookkeeping and h / c),
+// then the scores, the softmax's maximum m_s and sum z_s and the unnormalised context c_s of its range.
+// Each block publishes (m_s, z_s, c_s) with agent-scope stores and counts itself in; the last of the
+// utterance's blocks merges in split order: M = max m_s, w_s = exp(m_s - M), Z = sum w_s z_s,
+// ctx = (sum w_s c_s) / Z, and writes ctx (and its split words) as the unsplit form does.
+template <int KPB, int CELL = 0, bool TSPLIT = false>
 __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float* __restrict__ st, const float* __restrict__ qpart, const float* __restrict__ keysT,
     const float* __restrict__ ekT, const float* __restrict__ enc, const int32_t* __restrict__ lens,
@@ -121,6 +139,8 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   static_assert(CELL != 2 || KPB >= 2, "the folded beam step: beam rows of one utterance per block");
   static_assert(CELL != 3 || KPB == 4 || KPB == 8, "the fused beam select: one block per utterance, k = 4 or 8");
   static_assert(CELL != 4 || KPB == 4, "the fused beam select, two blocks per utterance: k = 8");
+  static_assert(!TSPLIT || CELL == 1, "the split attention: the folded greedy step");
+  constexpr int MAXG = TSPLIT ? AT_MAXG_SPLIT : AT_MAXG;
   // CELL 4 (round 5): KPB 4 at k = 8, so two blocks per utterance (B = 128: 256 blocks) run the same
   // select of step l - 1; the first (blockIdx.y == 0) does its global bookkeeping, both read their
   // rows' tokens and predecessor rows from their own copy
@@ -135,30 +155,33 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   // step l - 1 skips when every utterance finished before step l - 1; otherwise the block runs it and
   // the attention, whatever this launch's selects add to step l - 1's count)
   if (CELL != 1 && done_before(newdone, CELL >= 3 ? l - 1 : l) >= total) return;
-  const int Tq = attn_tq(Tp);
+  const int TqG = attn_tq(Tp);                 // keysT / ekT row stride
+  const int sp = TSPLIT ? (int)blockIdx.y : 0;  // the block's split
+  const int tbase = TSPLIT ? sp * cell.tc : 0;  // its first step
+  const int Tq = TSPLIT ? min(cell.tc, TqG - tbase) : TqG;  // its steps (a multiple of 4)
   float* qs = sm;                   // [AT_APAD][KPB]: q transposed, zero past A and for j >= nk
   float* eqs = qs + KPB * AT_APAD;  // [AT_APAD][KPB]: exp(2q) (split form), zero past A
   float* vs = eqs + KPB * AT_APAD;  // [A]
   float* v2s = vs + A;              // [A]: -2 v
   float* xs = v2s + A + AT_MAXG;    // scratch
-  float* es = xs + attn_scratch_floats<KPB>(Tq);  // [Tq][KPB]: one 4 x KPB-byte read per t
+  float* es = xs + attn_scratch_floats<KPB, MAXG>(Tq);  // [Tq][KPB]: one 4 x KPB-byte read per t
   float* hs = es + KPB * Tq;                       // CELL: [HD] h, then [AT_QS][A] query slices
   float* vl = hs + (CELL == 1 ? AT_CELL_FLOATS : 0);  // [npf][C]: value rows 0..npf-1 (LDS-DMA)
-  const int b = blockIdx.x, j0 = blockIdx.y * KPB;
+  const int b = blockIdx.x, j0 = TSPLIT ? 0 : blockIdx.y * KPB;
   const int nk = min(KPB, k - j0);
   // CELL 1: wv through readfirstlane, provably wave-uniform, so the prologue's per-wave roles are
   // scalar branches (blocks of their own for hipcc's wait insertion, not exec-masked regions whose
   // pending loads merge); the other instances keep the plain form (their register allocation)
   const int tid = threadIdx.x, wv = CELL == 1 ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6, ln = tid & 63;
-  const int len = min(lens[b], Tp);
+  const int len = TSPLIT ? max(0, min(min(lens[b], Tp) - tbase, Tq)) : min(lens[b], Tp);  // (local steps)
   const size_t row0 = (size_t)b * k + j0;
 
   // score work split (phase 2): G a-groups of apg keys rows x Tq / 4 chunks of 4 steps
   const int nch = Tq / 4;
-  const int G = min(AT_MAXG, max(1, AT_THREADS / nch));
+  const int G = min(MAXG, max(1, AT_THREADS / nch));
   const int apg = (A + G - 1) / G;
-  const float* kb = keysT + (size_t)b * A * Tq;
-  const float* ekb = ekT + (size_t)b * A * Tq;
+  const float* kb = keysT + (size_t)b * A * TqG + tbase;
+  const float* ekb = ekT + (size_t)b * A * TqG + tbase;
   constexpr int CH = KPB >= 8 ? AT_CH / 2 : AT_CH;  // KPB 8: half the keys rows per batch (registers)
   // CELL: the first keys batch of this thread's first score item (split form) is loaded before the
   // cell phase, which it does not depend on, so the scores start on landed keys
@@ -175,7 +198,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       const int tc = min(t0, Tq - 4);
 #pragma unroll
       for (int i = 0; i < CH; ++i)
-        kvp[i] = *reinterpret_cast<const float4*>(ekb + (size_t)min(a0 + i, A - 1) * Tq + tc);
+        kvp[i] = *reinterpret_cast<const float4*>(ekb + (size_t)min(a0 + i, A - 1) * TqG + tc);
       (void)live;
       (void)a1;
     } else {
@@ -270,7 +293,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
           const uint8_t fin0 = (uint8_t)__builtin_amdgcn_readfirstlane(finv);
           const float acc0 = __int_as_float(__builtin_amdgcn_readlane(bkv, 1));
           const int len0 = __builtin_amdgcn_readlane(bkv, 0);
-          if (ln == 0) {
+          if (ln == 0 && sp == 0) {  // (split: one block of the utterance writes the bookkeeping)
             if (bad_t) atomicOr(cell.err, CASR_DEV_NAN_LOGITS);
             greedy_book(gs, r, t, gm - (logf(sx) + gm), fin0, acc0, len0);
           }
@@ -312,9 +335,11 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     for (int g = 0; g < 4; ++g) eg[g] = hs[HD + gcol(g, u)];
     float h2, c2;
     lstm_cell_hw(gprev[0] + eg[0], gprev[1] + eg[1], gprev[2] + eg[2], gprev[3] + eg[3], cold, h2, c2);
-    st[(size_t)r * ST + C + u] = h2;
-    st[(size_t)r * ST + C + HD + u] = c2;
-    reinterpret_cast<uint32_t*>(st)[(size_t)r * ST + ST16 + C + u] = split16_word(h2);
+    if (sp == 0) {
+      st[(size_t)r * ST + C + u] = h2;
+      st[(size_t)r * ST + C + HD + u] = c2;
+      reinterpret_cast<uint32_t*>(st)[(size_t)r * ST + ST16 + C + u] = split16_word(h2);
+    }
     hs[u] = h2;
     __syncthreads();
     stamp(7);  // (diagnostics) the cell done, h in LDS
@@ -554,7 +579,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     auto load = [&](float4 (&kv)[CH], int ab) {
 #pragma unroll
       for (int i = 0; i < CH; ++i)
-        kv[i] = live && ab + i < a1 ? *reinterpret_cast<const float4*>(src + (size_t)(ab + i) * Tq + t0)
+        kv[i] = live && ab + i < a1 ? *reinterpret_cast<const float4*>(src + (size_t)(ab + i) * TqG + t0)
                                     : make_float4(0.f, 0.f, 0.f, 0.f);
     };
     int ab = a0;
@@ -597,7 +622,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): the keys batch has landed
     const uint32_t vbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)vl;
     for (int i = wv; i < 2 * nv; i += AT_WAVES) {  // 1 KB (half a row) per wave instruction
-      const float* src = enc + ((size_t)b * Tp + (i >> 1)) * C + (i & 1) * (C / 2) + 4 * ln;
+      const float* src = enc + ((size_t)b * Tp + tbase + (i >> 1)) * C + (i & 1) * (C / 2) + 4 * ln;
       const uint32_t dst = __builtin_amdgcn_readfirstlane(vbase + (uint32_t)i * (C / 2) * 4);
       uint32_t keep;
       asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
@@ -626,6 +651,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   // KPB <= 2 (greedy, k = 2): every thread takes a t and the reductions go through LDS (with one
   // or two rows a single wave's three lane-strided passes were slower: 2.3 against 1.2 us)
   static_assert(KPB <= AT_WAVES, "one wave per beam row of the block");
+  float m_split = -INFINITY, z_split = 0.f;  // TSPLIT: this block's softmax maximum and sum
   if constexpr (KPB <= 2) {
     __shared__ float wred[2][AT_WAVES][KPB];
     float lmax[KPB];
@@ -682,6 +708,11 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
       if (j < nk) {
         const float s = ((wred[1][0][j] + wred[1][1][j]) + (wred[1][2][j] + wred[1][3][j])) +
                         ((wred[1][4][j] + wred[1][5][j]) + (wred[1][6][j] + wred[1][7][j]));
+        if constexpr (TSPLIT) {  // the merge normalises: the context sums exp(e - m_s) v over the block's steps
+          m_split = len > 0 ? rmax[j] : -INFINITY;  // (a split past the utterance's end contributes nothing)
+          z_split = len > 0 ? s : 0.f;
+          continue;
+        }
         const float rinv = 1.0f / s;
         for (int t = tid; t < Tq; t += AT_THREADS) {
           const float al = es[t * KPB + j] * rinv;
@@ -726,7 +757,7 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
     float acc[KPB][4];
 #pragma unroll
     for (int j = 0; j < KPB; ++j) acc[j][0] = acc[j][1] = acc[j][2] = acc[j][3] = 0.f;
-    const float* eb = enc + (size_t)b * Tp * C + 4 * c4;
+    const float* eb = enc + ((size_t)b * Tp + tbase) * C + 4 * c4;
     // rows 0..nv-1 from LDS (the DMA issued in the score phase; nv is a multiple of 4 or len, so
     // each thread's t sequence continues unchanged into the global rows: same summation order)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -787,6 +818,71 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
   }
   stamp(4);
   __syncthreads();
+  if constexpr (TSPLIT) {
+    // publish (m_s, z_s, c_s) with agent-scope 8-byte stores (coherent across the XCDs' L2s), count
+    // in; the last of the utterance's cell.split blocks merges in split order (see the template note)
+    __shared__ int last_s;
+    const int S = cell.split;
+    auto slot = [&](int q) { return reinterpret_cast<uint64_t*>(cell.spart + ((size_t)b * AT_SPLIT_MAX + q) * (C + 4)); };
+    uint64_t* mine = slot(sp);
+    for (int i = tid; i < C / 4; i += AT_THREADS) {
+      const float4 p0 = *reinterpret_cast<const float4*>(xs + (0 * KPB) * C + 4 * i);
+      const float4 p1 = *reinterpret_cast<const float4*>(xs + (1 * KPB) * C + 4 * i);
+      const float4 p2 = *reinterpret_cast<const float4*>(xs + (2 * KPB) * C + 4 * i);
+      const float4 p3 = *reinterpret_cast<const float4*>(xs + (3 * KPB) * C + 4 * i);
+      const f32x2 lo = {(p0.x + p1.x) + (p2.x + p3.x), (p0.y + p1.y) + (p2.y + p3.y)};
+      const f32x2 hi = {(p0.z + p1.z) + (p2.z + p3.z), (p0.w + p1.w) + (p2.w + p3.w)};
+      __hip_atomic_store(mine + 2 * i, __builtin_bit_cast(uint64_t, lo), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(mine + 2 * i + 1, __builtin_bit_cast(uint64_t, hi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0)
+      __hip_atomic_store(mine + C / 2, __builtin_bit_cast(uint64_t, (f32x2){m_split, z_split}), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store retired before the count (gfx950: vmcnt
+                                                      // counts stores; decoder.hip's k-split note)
+    __syncthreads();
+    if (tid == 0) last_s = __hip_atomic_fetch_add(cell.scnt + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+    __syncthreads();
+    if (!last_s) {
+      stamp(5);  // (diagnostics) published and counted in
+      return;
+    }
+    float w[AT_SPLIT_MAX];
+    float M = -INFINITY, Z = 0.f;
+#pragma unroll
+    for (int q = 0; q < AT_SPLIT_MAX; ++q)
+      if (q < S) {
+        const f32x2 mz = __builtin_bit_cast(f32x2, __hip_atomic_load(slot(q) + C / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        w[q] = mz.x;
+        M = fmaxf(M, mz.x);
+      }
+#pragma unroll
+    for (int q = 0; q < AT_SPLIT_MAX; ++q)
+      if (q < S) {
+        const f32x2 mz = __builtin_bit_cast(f32x2, __hip_atomic_load(slot(q) + C / 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        w[q] = expf(w[q] - M);  // exp(-inf) = 0 for a split past the end
+        Z = q == 0 ? w[q] * mz.y : Z + w[q] * mz.y;
+      }
+    const float zinv = 1.0f / Z;
+    for (int i = tid; i < C / 4; i += AT_THREADS) {
+      f32x2 lo = {0.f, 0.f}, hi = {0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < AT_SPLIT_MAX; ++q)
+        if (q < S) {
+          const f32x2 a = __builtin_bit_cast(f32x2, __hip_atomic_load(slot(q) + 2 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          const f32x2 c = __builtin_bit_cast(f32x2, __hip_atomic_load(slot(q) + 2 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          lo = q == 0 ? w[q] * a : lo + w[q] * a;
+          hi = q == 0 ? w[q] * c : hi + w[q] * c;
+        }
+      const float4 cv = make_float4(lo.x * zinv, lo.y * zinv, hi.x * zinv, hi.y * zinv);
+      *reinterpret_cast<float4*>(st + row0 * ST + 4 * i) = cv;
+      *reinterpret_cast<u32x4*>(st + row0 * ST + ST16 + 4 * i) =
+          u32x4{split16_word(cv.x), split16_word(cv.y), split16_word(cv.z), split16_word(cv.w)};
+    }
+    if (tid == 0) __hip_atomic_store(cell.scnt + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    stamp(5);
+    return;
+  }
   for (int i = tid; i < nk * (C / 4); i += AT_THREADS) {
     const int j = i / (C / 4), c4 = i - j * (C / 4);
     const float4 p0 = *reinterpret_cast<const float4*>(xs + (0 * KPB + j) * C + 4 * c4);
@@ -808,9 +904,9 @@ __global__ __launch_bounds__(AT_THREADS) void attention_kernel(
 // budget (two blocks per CU) unchanged; the knob was removed in round 3.
 static size_t attn_lds_budget() { return (size_t)156 * 1024; }
 
-template <int KPB, int CELL = 0>
+template <int KPB, int CELL = 0, bool TSPLIT = false>
 static int attn_npf(int Tp) {
-  const size_t fixed = attn_smem_floats<KPB, CELL>(Tp) * sizeof(float);
+  const size_t fixed = attn_smem_floats<KPB, CELL, TSPLIT>(Tp) * sizeof(float);
   const size_t budget = attn_lds_budget();
   const size_t room = fixed < budget ? budget - fixed : 0;
   const int rows = (int)(room / (C * sizeof(float))) & ~3;
@@ -837,8 +933,31 @@ static hipError_t launch_kpb(const DecodeArgs& a, float* st, const float* qpart,
   return hipGetLastError();
 }
 
+// the split folded greedy attention (TSPLIT): cell.split blocks of cell.tc steps per utterance; the
+// LDS is sized for cell.tc steps
+static hipError_t launch_greedy_split(const DecodeArgs& a, float* st, int32_t* newdone, int l, int total,
+                                      hipStream_t s, const AttnCell& cell) {
+  if (cell.split < 2 || cell.split > AT_SPLIT_MAX || cell.tc < 4 || cell.tc % 4 || !cell.spart || !cell.scnt)
+    return hipErrorInvalidValue;
+  const int npf = attn_npf<1, 1, true>(cell.tc);
+  const size_t shm = (attn_smem_floats<1, 1, true>(cell.tc) + (size_t)npf * C) * sizeof(float);
+  static size_t raised = 0;
+  if (shm > raised) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(attention_kernel<1, 1, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+    raised = shm;
+  }
+  const float* ekT = a.keysT + (size_t)a.B * A * attn_tq(a.Tp);
+  hipLaunchKernelGGL((attention_kernel<1, 1, true>), dim3(a.B, cell.split), dim3(AT_THREADS), shm, s, st, nullptr,
+                     a.keysT, ekT, a.enc, a.lens, a.W + a.L.v, a.B, 1, a.Tp, nullptr, newdone, l, total, npf,
+                     a.attn_direct, dec_q_slots(a.B), a.V, cell);
+  return hipGetLastError();
+}
+
 hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const AttnCell& cell, float* align,
                                       int32_t* newdone, int l, int total, hipStream_t s) {
+  if (a.k == 1 && cell.split > 1 && !align) return launch_greedy_split(a, st, newdone, l, total, s, cell);
   if (a.k == 1) return launch_kpb<1, 1>(a, st, nullptr, align, newdone, l, total, s, cell);
   switch (attention_kpb(a.B, a.k, a.attn_kpb)) {
     case 4:

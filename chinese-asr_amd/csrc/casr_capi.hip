@@ -194,6 +194,7 @@ struct casr_handle {
   // decoder workspace
   DevBuf st, logits, small, bp, tk, rec, beam_small;
   DevBuf ksbuf;  // the greedy folded GEMM's k-split sums and counters (R <= 32, CASR_OPT_DEC_KSPLIT)
+  DevBuf asbuf;  // the split greedy attention's partials and counters (R <= 64, CASR_OPT_ATTN_SPLIT)
   DecodeBufs d{};
   DevBuf gout;  // internal decode outputs written by captured graphs
   Profiler prof;
@@ -540,7 +541,7 @@ void casr_destroy(casr_handle* h) {
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   for (DevBuf* b : {&h->gin, &h->out0, &h->out1, &h->hbuf, &h->cst, &h->hfin, &h->keysT, &h->lens, &h->feat, &h->fstat, &h->hx, &h->x16, &h->gflags, &h->fe_const,
                     &h->st, &h->logits, &h->small, &h->bp, &h->tk, &h->rec, &h->beam_small, &h->gout, &h->wfold, &h->wfold32, &h->coldbuf,
-                    &h->egates, &h->fgates, &h->wq16, &h->wih16km, &h->ksbuf})
+                    &h->egates, &h->fgates, &h->wq16, &h->wih16km, &h->ksbuf, &h->asbuf})
     b->release();
   delete h;
 }
@@ -574,8 +575,8 @@ int casr_recurrence_mode(const casr_handle* h, int B) {
 int casr_set_option(casr_handle* h, int option, int value) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
   if (option < 0 || option >= CASR_OPT_COUNT) return fail(h, CASR_ERR_ARG, "unknown option %d", option);
-  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 2, 2, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1, 1, 1, 1, 1, 1};
+  static const int lo[CASR_OPT_COUNT] = {0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  static const int hi[CASR_OPT_COUNT] = {1, 3, 1, 16, 8, 1, 2, 2, 8, 1, 1, CASR_MAX_LAYERS, (1 << CASR_K_COUNT) - 1, 1, 1, 1, 1, 1, AT_SPLIT_MAX};
   if (option == CASR_OPT_ATTN_KPB && value != 0 && value != 4 && value != 8)
     return fail(h, CASR_ERR_ARG, "CASR_OPT_ATTN_KPB: 0 (auto), 4 or 8");
   if (value < lo[option] || value > hi[option])
@@ -941,6 +942,17 @@ static int prepare_decode(casr_handle* h, int k, DecodeArgs& a, bool greedy) {
   d.rec_score = h->rec.as<float>();
   d.rec_src = reinterpret_cast<int32_t*>(d.rec_score + (size_t)B * L * k);
   d.rec_valid = reinterpret_cast<uint8_t*>(d.rec_src + (size_t)B * L * k);
+  d.aspart = nullptr;
+  d.ascnt = nullptr;
+  d.asplit = 0;
+  if (greedy && R <= 64 && h->tune[CASR_OPT_ATTN_SPLIT]) {
+    const size_t part = (size_t)R * AT_SPLIT_MAX * (C + 4) * sizeof(float);
+    HIP_OK(h, h->asbuf.ensure(part + (size_t)R * sizeof(int32_t)));
+    d.aspart = h->asbuf.as<float>();
+    d.ascnt = reinterpret_cast<int32_t*>(h->asbuf.as<char>() + part);
+    const int o = h->tune[CASR_OPT_ATTN_SPLIT];
+    d.asplit = o == 1 ? (R <= 32 ? 8 : 4) : o;  // 1: by R; 2..AT_SPLIT_MAX: that many
+  }
   d.kspart = nullptr;
   d.kscnt = nullptr;
   if (greedy && R <= 32 && h->tune[CASR_OPT_DEC_KSPLIT]) {
@@ -1022,7 +1034,7 @@ int casr_greedy(casr_handle* h, int32_t* tokens, int32_t* out_len, uint8_t* fini
   float* ial = align ? iacc + B : nullptr;
   uint8_t* ifin = reinterpret_cast<uint8_t*>(iacc + B + nal);
   a.prof = nullptr;
-  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)(h->d.kspart != nullptr), (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)a.fold, (uint64_t)h->fgates.p, (uint64_t)a.fb.wfold, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
+  const std::vector<uint64_t> key = {2, (uint64_t)a.s16, (uint64_t)(h->d.kspart != nullptr), (uint64_t)h->d.asplit, (uint64_t)h->asbuf.p, (uint64_t)a.fuse_select, (uint64_t)a.attn_kpb, (uint64_t)a.attn_direct, (uint64_t)a.fold, (uint64_t)h->fgates.p, (uint64_t)a.fb.wfold, (uint64_t)B, (uint64_t)h->Tp, (uint64_t)h->W, (uint64_t)h->gout.p,
                                      (uint64_t)(align != nullptr), (uint64_t)h->st.p, (uint64_t)h->logits.p,
                                      (uint64_t)h->small.p, (uint64_t)h->enc_out, (uint64_t)h->keysT.p,
                                      (uint64_t)h->hfin.p, (uint64_t)h->cst.p, (uint64_t)h->lens.p};

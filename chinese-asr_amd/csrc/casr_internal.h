@@ -71,7 +71,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1, 1, 0};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, 1, 2, 1, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1, 1, 0, 0};
   int operator[](int i) const { return v[i]; }
 };
 
@@ -409,6 +409,10 @@ struct DecodeBufs {
   // greedy at R <= 32 with CASR_OPT_DEC_KSPLIT: the k-range sums and arrival counters (else nullptr)
   float* kspart;         // [groups][2 waves][DG_KS][FOLD_NT tiles][64 lanes] x 4 floats
   int32_t* kscnt;
+  // greedy at R <= 64 with CASR_OPT_ATTN_SPLIT: the split attention's partials and counters (else nullptr)
+  float* aspart;         // [R][AT_SPLIT_MAX][C + 4]
+  int32_t* ascnt;        // [R]
+  int asplit;            // splits asked for (8 at R <= 32, 4 at R <= 64)
 };
 
 struct DecodeArgs {
@@ -457,7 +461,13 @@ struct AttnCell {
   GreedySel gs;
   int bsel;        // beam, one block per utterance: the select of step l - 1 runs in the prologue (bs)
   BeamSelArgs bs;
+  // greedy, CASR_OPT_ATTN_SPLIT (round 6): split > 1 blocks of tc steps per utterance, their
+  // (max, sum, context) partials [B][AT_SPLIT_MAX][C + 4] and per-utterance arrival counters
+  int split, tc;
+  float* spart;
+  int32_t* scnt;
 };
+constexpr int AT_SPLIT_MAX = 8;
 hipError_t launch_attention_cell_step(const DecodeArgs& a, float* st, const AttnCell& cell, float* align,
                                       int32_t* newdone, int l, int total, hipStream_t s);
 // fixed LDS of the attention launch; cell = 1: the folded greedy step's attention_kernel<1, 1>

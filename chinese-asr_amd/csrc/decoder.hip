@@ -1709,6 +1709,12 @@ static hipError_t fold_attention_step(const DecodeArgs& a, DecodeBufs& d, int l,
   if (bs) {
     cell.bsel = 1;
     cell.bs = *bs;
+  } else if (d.aspart && !align) {  // greedy, CASR_OPT_ATTN_SPLIT: d.asplit ranges of a multiple of 4 steps
+    const int tq = (a.Tp + 3) & ~3;  // (attention.hip's attn_tq)
+    cell.tc = ((tq + d.asplit - 1) / d.asplit + 3) & ~3;
+    cell.split = (tq + cell.tc - 1) / cell.tc;  // (< 2 at short inputs: the unsplit form)
+    cell.spart = d.aspart;
+    cell.scnt = d.ascnt;
   }
   return launch_attention_cell_step(a, d.st[(l + 1) & 1], cell, align, d.newdone, l, total, s);
 }
@@ -1752,6 +1758,7 @@ hipError_t run_greedy(const DecodeArgs& a_in, DecodeBufs& d, int32_t* tokens, in
   fl.add32(accum, 0, R);
   fl.add32(tokens, 0xffffffffu, (size_t)R * a.max_len);
   if (d.kscnt) fl.add32(d.kscnt, 0, DG_KS_COUNTERS);
+  if (d.ascnt) fl.add32(d.ascnt, 0, R);
   hipError_t e0 = fill_multi(fl, s);
   if (e0 != hipSuccess) return e0;
   if (a.fold) return run_greedy_fold(a, d, tokens, out_len, finished, accum, align, s);

@@ -292,6 +292,14 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            last bits (within the 2e-3 score tolerance), and at a near tie of two
  *                            beam candidates their rank can differ from an expf build's
  *   CASR_LOGITS_NT           (decoder.hip) beam logits stored with the non-temporal hint: speed only
+ *   CASR_OPT_ATTN_SPLIT      0 (default): one attention block per utterance.  1 (round 6, measured and
+ *                            not adopted): the folded greedy attention at R <= 64
+ *                            decode rows (BASELINE config 2) splits each utterance's time steps over 8
+ *                            (R <= 32) or 4 blocks, whose softmax maxima, sums and unnormalised
+ *                            contexts the last block merges in split order (the same token ids; scores
+ *                            within 1e-4 of the unsplit form, test_greedy_split_attention_small_batch);
+ *                            2..8: that many ranges at every R <= 64.  Not with an alignment output
+ *                            (it needs the whole row)
  * One option exists for tests only:
  *   CASR_OPT_REC_COOP_REFUSE 0 (default): off; n in 1..8: casr_encode treats the cooperative launch
  *                            of encoder layer n - 1 as refused (hipErrorCooperativeLaunchTooLarge,
@@ -324,7 +332,8 @@ enum {
   CASR_OPT_X16_KM = 15,
   CASR_OPT_DEC_KSPLIT = 16,
   CASR_OPT_GEMM16_LEAN = 17,
-  CASR_OPT_COUNT = 18
+  CASR_OPT_ATTN_SPLIT = 18,
+  CASR_OPT_COUNT = 19
 };
 int casr_set_option(casr_handle* h, int option, int value);
 int casr_get_option(const casr_handle* h, int option, int32_t* value_host);

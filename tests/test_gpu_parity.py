@@ -896,3 +896,47 @@ def test_greedy_ksplit_small_batch(eng, B, graphs):
     r = O.greedy_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd)
     assert toks == r["tokens"]
     np.testing.assert_allclose(score, r["score"], atol=2e-3, rtol=0)
+
+
+@pytest.mark.parametrize("B,graphs", [(1, False), (19, True), (32, False), (32, True), (64, True)])
+def test_greedy_split_attention_small_batch(eng, B, graphs):
+    """BASELINE config 2's decode rows (R <= 64): the folded greedy attention with each utterance's
+    time steps split over 8 (R <= 32) or 4 workgroups (CASR_OPT_ATTN_SPLIT = 1; off by default,
+    DESIGN 9d item 5; the last to arrive merges the ranges' softmax maxima, sums and unnormalised contexts in split order)
+    against one workgroup per utterance.  Ragged lengths from 60 to 800 frames, so the later ranges
+    of the short utterances hold no step at all.  Tokens identical, scores within 1e-4, both equal
+    to the CPU oracle's tokens, the split path bitwise stable over repeated runs (graph replays
+    included) and its arrival counters left at zero (a second decode matches the first)."""
+    enc_sd, dec_sd = synthetic_state_dicts(CFG, peaked=True)
+    eng.bind(pack_weights(CFG, enc_sd, dec_sd))
+    rs = np.random.RandomState(100 + B)
+    frames = [800] if B == 1 else [800, 60] + rs.randint(60, 801, size=B - 2).tolist()
+    fb, fr = batch_fbank(frames, eng.device)
+    eng.encode_fbank(fb, fr)
+    eng.set_graphs(3 if graphs else 2)
+    res = {}
+    try:
+        for sp in (0, 1):
+            eng.set_option("ATTN_SPLIT", sp)
+            runs = []
+            for _ in range(3):
+                out = eng.greedy()
+                assert eng.device_flags() == 0
+                runs.append({k: v.cpu().clone() for k, v in out.items() if torch.is_tensor(v)})
+            for r2 in runs[1:]:
+                for k in runs[0]:
+                    assert torch.equal(runs[0][k], r2[k]), k
+            res[sp] = runs[0]
+    finally:
+        eng.set_option("ATTN_SPLIT", 0)
+        eng.set_graphs(2)
+    a, b = res[0], res[1]
+    assert torch.equal(a["tokens"], b["tokens"])
+    assert torch.equal(a["out_len"], b["out_len"])
+    np.testing.assert_allclose(b["accum"].numpy(), a["accum"].numpy(), atol=1e-4, rtol=0)
+    toks, score = greedy_outputs(b["tokens"].numpy(), b["out_len"].numpy(), b["finished"].numpy().astype(bool),
+                                 b["accum"].numpy())
+    feats = [O.features_from_fbank(fbank_for(i, t)) for i, t in enumerate(frames)]
+    r = O.greedy_decode(feats, [f.shape[0] for f in feats], enc_sd, dec_sd)
+    assert toks == r["tokens"]
+    np.testing.assert_allclose(score, r["score"], atol=2e-3, rtol=0)
