@@ -220,6 +220,8 @@ def main():
     ap.add_argument("--beam-streams", type=int, default=2, help="batches in flight for the metric's beam line")
     ap.add_argument("--config2-streams", type=int, default=4,
                     help="BASELINE config 2's pipelined side measurement (its line itself is one batch in flight)")
+    ap.add_argument("--no-s16x1", action="store_true",
+                    help="skip config 2's opt-in s16x1 perf-arithmetic side measurement (libcasr_hip_s16x1.so)")
     ap.add_argument("--graphs", type=int, default=0,
                     help="1: hipGraph replay of the decode loop (casr_set_graphs); default 0: eager launches")
     args = ap.parse_args()
@@ -462,6 +464,60 @@ def main():
             config3 = beam_line(args.config3_batch, args.beam, args.beam_steps, "config3", n=1)
             config3["config"] = "BASELINE config 3 (config 4 at --gpus 8): beam 8, B=128/GPU, T=800"
 
+    def s16x1_line(fbs, frs):
+        """BASELINE config 2's opt-in perf arithmetic (include/casr.h CASR_PREC_S16X1, SURVEY 7(ii):
+        one f16 MFMA per split product, the libcasr_hip_s16x1.so build) on the same B = 32 batch, one
+        batch in flight.  Its token ids are compared with this line's s16x3 ones of the same batch
+        (which tests/test_gpu_scale.py pins to the oracle on every row): reported, not claimed equal."""
+        from casr.engine import Engine
+        from casr.results import greedy_outputs
+        Bs = fbs.shape[0]
+
+        def run(e):
+            e.encode_fbank(fbs, frs)
+            return e.greedy()
+
+        def seqs(o):
+            o = {k: v.cpu().numpy() for k, v in o.items() if torch.is_tensor(v)}
+            return greedy_outputs(o["tokens"], o["out_len"], o["finished"].astype(bool), o["accum"])[0]
+
+        ref = seqs(run(eng))
+        e1 = Engine(cfg, packed=packed, device=dev, arithmetic="s16x1")
+        try:
+            e1.set_graphs(2 | (1 if args.graphs else 0))
+            assert e1.precision() == "s16x1", e1.precision()
+            run(e1)
+            e1.device_flags()
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                to_host(run(e1)["tokens"], "s16x1")
+            torch.cuda.synchronize()
+            barrier()
+            dt1 = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            if dist is not None:
+                dist.all_reduce(dt1, op=dist.ReduceOp.MAX)
+            flags["config2_s16x1"] = e1.device_flags()
+            e1.profile(CLASSES)
+            got = seqs(run(e1))
+            bd1 = e1.profile_read()
+            e1.profile([])
+        finally:
+            e1.close()
+        same = sum(a == b for a, b in zip(ref, got))
+        pos = sum(max(len(a), len(b)) for a, b in zip(ref, got))
+        hit = sum(sum(x == y for x, y in zip(a, b)) for a, b in zip(ref, got))
+        dt1 = float(dt1.item())
+        return {"arithmetic": "s16x1 (hi.hi f16 MFMA only, f32 accumulate; opt-in, never the headline)",
+                "value": Bs * world * args.steps / dt1, "unit": "utt/s", "ms_per_step": 1000.0 * dt1 / args.steps,
+                "kernel_breakdown_ms": {c: round(v[1], 3) for c, v in bd1.items()},
+                "token_agreement": {"against": "s16x3 token ids of the same batch (= the oracle's, "
+                                               "tests/test_gpu_scale.py test_config2_greedy_b32_matches_oracle)",
+                                    "utterances_identical": same, "utterances": len(ref),
+                                    "token_positions_equal": hit, "token_positions": pos,
+                                    "rate": hit / max(pos, 1)}}
+
     # BASELINE config 2: a B = 32 greedy batch (same weights, same step)
     small = None
     if not args.no_configs:
@@ -499,6 +555,8 @@ def main():
                                   "note": "throughput with nc2 B = 32 batches in flight on nc2 handles / streams; "
                                           "ms_per_step is wall time per batch, device_ms_per_step each batch's own "
                                           "span (its latency under the overlap)".replace("nc2", str(nc2))}
+        if precision == "s16x3" and not args.no_s16x1:
+            small["s16x1_perf_mode"] = s16x1_line(fbs, frs)
 
     # BASELINE config 1: one 8 s WAV, greedy, through the drop-in main.parse (main.py:27-65):
     # 16 kHz samples on the host -> log-mel, delta / stack / CMVN -> encoder -> greedy -> text.

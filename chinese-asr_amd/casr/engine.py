@@ -17,7 +17,7 @@ from .config import CasrConfig
 
 # casr_device_flags guard bits (include/casr.h) that invalidate results
 FLAG_REC_TIMEOUT = 32   # a persistent-recurrence hand-off wait expired: that encode is invalid
-FLAG_F16_RANGE = 128    # s16x3: an activation beyond the f16 range, the split images are wrong
+FLAG_F16_RANGE = 128    # s16x3 / s16x1: an activation beyond the f16 range, the split images are wrong
 
 
 def _ptr(t):
@@ -44,18 +44,23 @@ def _close_all():
 
 
 class Engine:
-    """casr handle bound to packed weights on one device."""
+    """casr handle bound to packed weights on one device.
 
-    def __init__(self, cfg: CasrConfig, enc_sd=None, dec_sd=None, device=None, packed=None):
+    arithmetic: "s16x3" (default, the shipped library) or "s16x1", the opt-in perf arithmetic of
+    the libcasr_hip_s16x1.so build (include/casr.h CASR_PREC_S16X1: one f16 MFMA per split
+    product; token ids not identical to the reference's).  Either can run "f32" by set_precision."""
+
+    def __init__(self, cfg: CasrConfig, enc_sd=None, dec_sd=None, device=None, packed=None, arithmetic="s16x3"):
         if not torch.cuda.is_available():
             raise _lib.CasrError("casr Engine needs an MI355X GPU (torch.cuda.is_available() is False)")
         self.cfg = cfg
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else
                                    torch.device(device).index or 0)
-        self.lib = _lib.load()
+        self.lib = _lib.load(variant=_lib.VARIANT_OF[arithmetic])
         self.handle = ctypes.c_void_p()
         c = _lib.config_struct(cfg)
-        _lib.check(self.lib.casr_create(ctypes.byref(c), self.device.index, ctypes.byref(self.handle)))
+        _lib.check(self.lib.casr_create(ctypes.byref(c), self.device.index, ctypes.byref(self.handle)), lib=self.lib)
+        _lib.register_handle(self.handle, self.lib)
         _LIVE.add(self)
         self.packed = None
         if packed is None and enc_sd is not None:
@@ -63,7 +68,7 @@ class Engine:
         if packed is not None:  # no weights: front-end only (log_mel / features)
             self.bind(packed)
         self._B = self._Tp = None
-        self.requested = "s16x3"
+        self.requested = arithmetic
         # A/B tooling hook (tools/probes): CASR_OPTS="REC_SLEEP=2,REC_POLL_GAP=3" sets tuning
         # options on every new handle; the library itself reads no environment
         for item in filter(None, os.environ.get("CASR_OPTS", "").split(",")):
@@ -87,6 +92,7 @@ class Engine:
     def close(self):
         """Destroy the handle (casr_destroy drains the device first).  Idempotent."""
         if self.handle:
+            _lib.unregister_handle(self.handle)
             self.lib.casr_destroy(self.handle)
             self.handle = ctypes.c_void_p()
         _LIVE.discard(self)
@@ -222,7 +228,8 @@ class Engine:
         _lib.check(self.lib.casr_set_persistent(self.handle, int(bool(enable))), self.handle)
 
     def set_precision(self, precision):
-        """'s16x3' (default: split-f16 MFMA, f32 accumulate) or 'f32' (exact-f32 MFMA)."""
+        """'s16x3' (default: split-f16 MFMA, f32 accumulate) or 'f32' (exact-f32 MFMA); an
+        Engine(arithmetic='s16x1') takes 's16x1' or 'f32'."""
         _lib.check(self.lib.casr_set_precision(self.handle, _lib.PRECISIONS[precision]), self.handle)
         self.requested = precision
 
@@ -246,7 +253,7 @@ class Engine:
         encode()
         out = decode()
         f = self.check_flags()
-        if f & FLAG_F16_RANGE and self.precision() == "s16x3":
+        if f & FLAG_F16_RANGE and self.precision() in ("s16x3", "s16x1"):
             req = self.requested
             self.set_precision("f32")
             try:
@@ -268,7 +275,7 @@ class Engine:
         return v.value
 
     def precision(self):
-        """Effective arithmetic of the MFMA contractions ('s16x3' or 'f32')."""
+        """Effective arithmetic of the MFMA contractions ('s16x3', 's16x1' or 'f32')."""
         p = int(self.lib.casr_get_precision(self.handle))
         return {v: k for k, v in _lib.PRECISIONS.items()}[p]
 

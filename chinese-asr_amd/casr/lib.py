@@ -25,8 +25,10 @@ EXPORTS = [
     "casr_set_option", "casr_get_option",
 ]
 
-# arithmetic of the MFMA contractions (casr_set_precision)
-PRECISIONS = {"f32": 0, "s16x3": 1}
+# arithmetic of the MFMA contractions (casr_set_precision); s16x1 is the opt-in perf arithmetic of
+# the libcasr_hip_s16x1.so build (build.py variant "s16x1"), which Engine(arithmetic="s16x1") loads
+PRECISIONS = {"f32": 0, "s16x3": 1, "s16x1": 2}
+VARIANT_OF = {"s16x3": None, "s16x1": "s16x1"}
 
 # tuning options (include/casr.h CASR_OPT_*): speed only, every value gives the same bits, except
 # ATTN_DIRECT (the direct tanh(k + q) attention scores) and DEC_FOLD (the folded decode step: two
@@ -68,19 +70,21 @@ class CasrError(RuntimeError):
     pass
 
 
-_LIB = None
+_LIBS = {}     # variant -> loaded library
+_HANDLES = {}  # casr handle address -> the library that created it (check() reads its error text)
 
 
-def load(path=None):
-    """Load (building first if stale and a compiler is present) the HIP library."""
-    global _LIB
-    if _LIB is not None:
-        return _LIB
+def load(path=None, variant=None):
+    """Load (building first if stale and a compiler is present) the HIP library: the shipped
+    build, or variant "s16x1" (the opt-in perf arithmetic)."""
+    key = path or variant
+    if key in _LIBS:
+        return _LIBS[key]
     import torch  # noqa: F401  (HIP runtime first)
-    path = path or _build.LIB
-    if not os.path.exists(path) or _build.is_stale():
+    path = path or _build.lib_path(variant)
+    if not os.path.exists(path) or _build.is_stale(variant):
         if os.path.exists(_build.HIPCC):
-            _build.build()
+            _build.build(variant=variant)
         if not os.path.exists(path):
             raise CasrError(f"casr HIP library not found at {path}; run __graft_entry__.build()")
     lib = ctypes.CDLL(path)
@@ -121,13 +125,22 @@ def load(path=None):
         fn.argtypes = args
     if lib.casr_api_version() != 3:
         raise CasrError("casr library API version mismatch")
-    _LIB = lib
+    _LIBS[key] = lib
     return lib
 
 
-def check(rc, handle=None):
+def register_handle(handle, lib):
+    _HANDLES[handle.value] = lib
+
+
+def unregister_handle(handle):
+    _HANDLES.pop(handle.value, None)
+
+
+def check(rc, handle=None, lib=None):
     if rc != 0:
-        msg = load().casr_last_error(handle)
+        lib = lib or (_HANDLES.get(handle.value) if handle is not None and handle.value else None) or load()
+        msg = lib.casr_last_error(handle)
         raise CasrError(f"{STATUS.get(rc, rc)}: {msg.decode(errors='replace') if msg else ''}")
 
 

@@ -170,7 +170,7 @@ struct casr_handle {
   DevBuf gflags;
   DevBuf fe_const; // FrontendConst (filterbank, window, twiddles), built on first casr_log_mel
   bool use_persistent = true;
-  int precision = CASR_PREC_S16X3;  // requested (casr_set_precision)
+  int precision = CASR_PREC_S16;  // requested (casr_set_precision)
   bool s16_valid = false;           // the bound blob's s16 images are usable (Layout::info)
   bool proj_small = false;          // every |W_p| < 16 (Layout::info + 4)
   bool dec_small = false;           // every decoder LSTM weight < 16 (Layout::info + 5)
@@ -187,7 +187,7 @@ struct casr_handle {
   DevBuf wfold32;
   DevBuf coldbuf;  // CASR_OPT_DIAG_COLD's flush source (measurement only)
   bool fold32_ready = false;
-  bool s16() const { return precision == CASR_PREC_S16X3 && s16_valid; }
+  bool s16() const { return precision == CASR_PREC_S16 && s16_valid; }
   int B = 0, Tp = 0;
   bool encoded = false;
   float* enc_out = nullptr;  // out0 or out1
@@ -514,15 +514,18 @@ static int ensure_fold32(casr_handle* h) {
 
 int casr_set_precision(casr_handle* h, int precision) {
   if (!h) return fail(h, CASR_ERR_ARG, "handle NULL");
-  if (precision != CASR_PREC_F32 && precision != CASR_PREC_S16X3)
+  if (precision != CASR_PREC_F32 && precision != CASR_PREC_S16X3 && precision != CASR_PREC_S16X1)
     return fail(h, CASR_ERR_ARG, "unknown precision %d", precision);
+  if (precision != CASR_PREC_F32 && precision != CASR_PREC_S16)
+    return fail(h, CASR_ERR_UNSUPPORTED, "this build computes %s; %s is the %s build", CASR_S16_ONE ? "s16x1" : "s16x3",
+                CASR_S16_ONE ? "s16x3" : "s16x1", CASR_S16_ONE ? "libcasr_hip.so" : "libcasr_hip_s16x1.so");
   h->precision = precision;
   return CASR_OK;
 }
 
 int casr_get_precision(const casr_handle* h) {
   if (!h) return -1;
-  return h->s16() ? CASR_PREC_S16X3 : CASR_PREC_F32;
+  return h->s16() ? CASR_PREC_S16 : CASR_PREC_F32;
 }
 
 void casr_destroy(casr_handle* h) {

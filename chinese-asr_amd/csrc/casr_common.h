@@ -65,11 +65,23 @@ CASR_DEV void unpack16_tagged(u32x4 w0, u32x4 w1, f16x8& hi, f16x8& lo) {
   lo = __builtin_bit_cast(f16x8, l);
 }
 
-// three MFMAs of one s16x3 product into the (hi.hi, cross) accumulator pair
+// CASR_S16_ONE = 1 is the s16x1 build (libcasr_hip_s16x1.so, casr/build.py; round 6, BASELINE
+// config 2's opt-in perf arithmetic, CASR_PREC_S16X1): every split product keeps its hi.hi MFMA
+// only, the two cross-term MFMAs of each site are compiled out (11 significant operand bits
+// instead of 22; the same images, bytes and code otherwise).  The shipped library is built
+// without it.
+#ifndef CASR_S16_ONE
+#define CASR_S16_ONE 0
+#endif
+constexpr bool kS16Cross = !CASR_S16_ONE;
+
+// three MFMAs of one s16x3 product into the (hi.hi, cross) accumulator pair (s16x1: the first)
 CASR_DEV void mfma_s16(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x4& hh, f32x4& x) {
   hh = mfma16x16x32h(ah, bh, hh);
-  x = mfma16x16x32h(ah, bl, x);
-  x = mfma16x16x32h(al, bh, x);
+  if constexpr (kS16Cross) {
+    x = mfma16x16x32h(ah, bl, x);
+    x = mfma16x16x32h(al, bh, x);
+  }
 }
 
 CASR_DEV float s16_combine(float hh, float x) { return hh + x * S16_LO_INV; }

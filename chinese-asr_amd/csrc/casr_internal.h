@@ -8,6 +8,12 @@
 
 #include "casr.h"
 
+// the s16 arithmetic of this build (casr_common.h CASR_S16_ONE: the s16x1 build)
+#ifndef CASR_S16_ONE
+#define CASR_S16_ONE 0
+#endif
+constexpr int CASR_PREC_S16 = CASR_S16_ONE ? CASR_PREC_S16X1 : CASR_PREC_S16X3;
+
 namespace casr {
 
 // Dimensions of the deployed configuration (gpd.py), fixed at compile time so every

@@ -339,8 +339,10 @@ __global__ __launch_bounds__(512, 2) void dgemm_kernel(int NB, int NR, int ntile
 #pragma unroll
             for (int rs = 0; rs < RS; ++rs) {
               acc[rs][tn] = mfma16x16x32h(ah[rs], b1, acc[rs][tn]);
-              acc[rs][tn] = mfma16x16x32h(ah[rs], bl, acc[rs][tn]);
-              acc[rs][tn] = mfma16x16x32h(al[rs], bh, acc[rs][tn]);
+              if constexpr (kS16Cross) {
+                acc[rs][tn] = mfma16x16x32h(ah[rs], bl, acc[rs][tn]);
+                acc[rs][tn] = mfma16x16x32h(al[rs], bh, acc[rs][tn]);
+              }
             }
           } else {
 #pragma unroll

@@ -117,8 +117,10 @@ __global__ __launch_bounds__(64 * MH * WN, WN* MH / 4) void gemm16_bias_kernel(c
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w1[t], acc[tm][t], 0, 0, 0);
-          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl[t], acc[tm][t], 0, 0, 0);
-          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh[t], acc[tm][t], 0, 0, 0);
+          if constexpr (kS16Cross) {
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl[t], acc[tm][t], 0, 0, 0);
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh[t], acc[tm][t], 0, 0, 0);
+          }
         }
       }
     }
@@ -275,8 +277,10 @@ __global__ __launch_bounds__(512, 2) void gemm16_persist_kernel(const float* __r
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w1[t], acc[tm][t], 0, 0, 0);
-          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl[t], acc[tm][t], 0, 0, 0);
-          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh[t], acc[tm][t], 0, 0, 0);
+          if constexpr (kS16Cross) {
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl[t], acc[tm][t], 0, 0, 0);
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh[t], acc[tm][t], 0, 0, 0);
+          }
         }
       });
     });
@@ -573,8 +577,10 @@ __global__ __launch_bounds__(512, 2) void gemm16_pp_kernel(const float* __restri
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
             acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], w1[t], acc[tm][t], 0, 0, 0);
-            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], wl[t], acc[tm][t], 0, 0, 0);
-            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[tm], wh[t], acc[tm][t], 0, 0, 0);
+            if constexpr (kS16Cross) {
+              acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], wl[t], acc[tm][t], 0, 0, 0);
+              acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[tm], wh[t], acc[tm][t], 0, 0, 0);
+            }
           }
       } else {
         if (ah[0][0] == (_Float16)1234.f && wh[0][0] == (_Float16)4321.f) acc[0][0][0] += 1.f;
@@ -790,8 +796,10 @@ __global__ __launch_bounds__(512, 2) void gemm16_pp_lean_kernel(const float* __r
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], w1[t], acc[tm][t], 0, 0, 0);
-          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], wl[t], acc[tm][t], 0, 0, 0);
-          acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[tm], wh[t], acc[tm][t], 0, 0, 0);
+          if constexpr (kS16Cross) {
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[tm], wl[t], acc[tm][t], 0, 0, 0);
+            acc[tm][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[tm], wh[t], acc[tm][t], 0, 0, 0);
+          }
         }
       __builtin_amdgcn_s_setprio(0);
       if (grp == 0 && j + 1 < nk) vwait();
@@ -941,8 +949,10 @@ __global__ __launch_bounds__(256, 1) void gemm16_tail_kernel(const float* __rest
         const f16x8 ah = frag(row, false);
         const f16x8 al = frag(row, true);
         acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, w1, acc[tm], 0, 0, 0);
-        acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl, acc[tm], 0, 0, 0);
-        acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh, acc[tm], 0, 0, 0);
+        if constexpr (kS16Cross) {
+          acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, wl, acc[tm], 0, 0, 0);
+          acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, wh, acc[tm], 0, 0, 0);
+        }
       }
     }
   };

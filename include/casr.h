@@ -198,10 +198,18 @@ int casr_set_persistent(casr_handle* h, int enable);
  *   CASR_PREC_S16X3  every f32 operand split as hi + 2^-11 lo (two f16), three f16 MFMAs per
  *                    product (hi.hi + 2^-11 (hi.lo + lo.hi)) on the 16x-faster f16 pipes; 22
  *                    significant operand bits, measured error no larger than the f32 path's.
- * Default S16X3.  A blob whose MFMA weights do not fit the split (non-finite, |w| >= 2^14, or
- * an encoder W_ih entry >= 16) runs F32 whatever is set; casr_get_precision reports the
- * effective mode. */
-enum { CASR_PREC_F32 = 0, CASR_PREC_S16X3 = 1 };
+ *   CASR_PREC_S16X1  (round 6, an opt-in perf arithmetic, never the headline: BASELINE config 2's
+ *                    "bf16 perf mode") the hi.hi MFMA of every split product only:
+ *                    one f16 MFMA instead of three, 11 significant operand bits (bf16 keeps 8),
+ *                    f32 accumulators.  Token ids are NOT identical to the reference's; bench.py
+ *                    reports its token agreement.  It is a separate build of this library,
+ *                    libcasr_hip_s16x1.so (casr/build.py variant "s16x1", -DCASR_S16_ONE=1), whose
+ *                    s16 mode is S16X1: each build accepts F32 and its own s16 mode, and answers
+ *                    the other s16 mode with CASR_ERR_UNSUPPORTED.
+ * Default: the build's s16 mode.  A blob whose MFMA weights do not fit the split (non-finite,
+ * |w| >= 2^14, or an encoder W_ih entry >= 16) runs F32 whatever is set; casr_get_precision
+ * reports the effective mode. */
+enum { CASR_PREC_F32 = 0, CASR_PREC_S16X3 = 1, CASR_PREC_S16X1 = 2 };
 int casr_set_precision(casr_handle* h, int precision);
 int casr_get_precision(const casr_handle* h); /* effective mode, -1 on a NULL handle */
 

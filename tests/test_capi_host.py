@@ -30,6 +30,22 @@ def test_library_exports_every_header_symbol():
     assert lib.casr_api_version() == 3
 
 
+def test_s16x1_build_exports_the_same_symbols_and_layout():
+    """The opt-in s16x1 perf arithmetic is a second build of the same sources (casr/build.py
+    variant "s16x1", include/casr.h CASR_PREC_S16X1): the same exports, API version and packed
+    blob (a blob packed by either library binds to both)."""
+    base, var = L.load(), L.load(variant="s16x1")
+    assert base is not var
+    for name in header_functions():
+        assert hasattr(var, name), name
+    assert var.casr_api_version() == 3
+    c = L.config_struct(CFG)
+    assert var.casr_packed_weights_floats(ctypes.byref(c)) == base.casr_packed_weights_floats(ctypes.byref(c))
+    hdr = open(os.path.join(REPO, "include", "casr.h")).read()
+    precs = dict((m.group(1).lower(), int(m.group(2))) for m in re.finditer(r"CASR_PREC_([A-Z0-9]+) = (\d+)", hdr))
+    assert precs == L.PRECISIONS
+
+
 def test_create_without_gpu_or_bad_config_fails_loudly():
     import torch
     lib = L.load()
