@@ -46,6 +46,25 @@ def test_s16x1_build_exports_the_same_symbols_and_layout():
     assert precs == L.PRECISIONS
 
 
+def test_check_reads_the_error_text_of_the_handle_s_library():
+    """casr.lib.check on a handle asks the library that created it (an s16x1 Engine's handle is
+    not the shipped library's); without a handle, the given library or the shipped one."""
+    var = L.load(variant="s16x1")
+    bad = L.config_struct(CFG)
+    bad.enc_hidden = 128
+    h = ctypes.c_void_p()
+    rc = var.casr_create(ctypes.byref(bad), 0, ctypes.byref(h))
+    with pytest.raises(L.CasrError, match="enc_hidden"):
+        L.check(rc, lib=var)
+    fake = ctypes.c_void_p(0x1000)
+    L.register_handle(fake, var)
+    try:
+        assert L._HANDLES[fake.value] is var
+    finally:
+        L.unregister_handle(fake)
+    assert fake.value not in L._HANDLES
+
+
 def test_create_without_gpu_or_bad_config_fails_loudly():
     import torch
     lib = L.load()
