@@ -35,6 +35,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "casr_common.h"
 #include "casr_internal.h"
 
@@ -471,6 +473,22 @@ hipError_t reset_rec_layer(uint32_t* hx, int B, int layout, hipStream_t s) {
   return fill_multi(fl, s);
 }
 
+// CASR_OPT_REC_COOP 2 (default, round 6): the persistent layer is an ordinary launch, ordered after
+// the previous persistent launch of this process on the same device by one process-wide event per
+// device (its stream waits for that event, the launch records it).  The hand-off spins need every
+// workgroup of the grid resident: two persistent grids dispatched side by side (batches in flight
+// on several streams, casr/pipeline.py) could each hold part of the chip and wait on the other, so
+// they never overlap; any other kernel beside a partly placed grid finishes and frees its CUs.  The
+// cooperative launch (1) gave the same guarantee at about 25 us per launch (interleaved A/B,
+// profiles/r06/rec_launch/: greedy 6.53-6.58 -> 6.43-6.46 ms per batch serially, beam 10.11-10.13
+// -> 9.99-10.06 ms with two in flight).  Another process's persistent grid is not ordered: the
+// bounded hand-off wait (device flag 32) covers that case, as for the ordinary launch (0).
+namespace {
+std::mutex g_rec_chain_mu;
+constexpr int REC_CHAIN_DEVICES = 64;
+hipEvent_t g_rec_chain[REC_CHAIN_DEVICES] = {};
+}  // namespace
+
 hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* xin, float* out,
                             uint16_t* x16, uint32_t* hx, float* hfin, float* cst, const int32_t* lens, int B, int Tp,
                             int residual, int s16, int32_t* err, uint32_t* trace, int layout, const Tuning& t,
@@ -483,15 +501,36 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
   int plain = t[CASR_OPT_REC_STORE_PLAIN] ? 1 : 0;
   const dim3 grid((H / UW) * nrg * 2), block(RG * UW);
   auto go = [&](auto kern) -> hipError_t {
-    if (t[CASR_OPT_REC_COOP]) {
+    if (t[CASR_OPT_REC_COOP] == 1) {
       // every workgroup co-resident or an immediate launch error (the hand-off spins need all of them)
       void* args[] = {&Whh_f, &Gin, &xin, &out, &x16, &hx, &hfin, &cst, &lens, &B, &Bp, &Tp, &residual,
                       &err, &trace, &nrg, &sleep, &gap, &plain, &km};
       return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kern), grid, block, args, 0, s);
     }
+    hipEvent_t chain = nullptr;
+    std::unique_lock<std::mutex> lk(g_rec_chain_mu, std::defer_lock);
+    if (t[CASR_OPT_REC_COOP] == 2) {  // ordered after this process's previous persistent grid (above)
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      int dev = -1;
+      hipError_t e = hipStreamIsCapturing(s, &cs);
+      if (e == hipSuccess) e = hipGetDevice(&dev);
+      if (e != hipSuccess) return e;
+      if (cs == hipStreamCaptureStatusNone && dev >= 0 && dev < REC_CHAIN_DEVICES) {
+        lk.lock();
+        if (!g_rec_chain[dev]) {
+          e = hipEventCreateWithFlags(&g_rec_chain[dev], hipEventDisableTiming);
+          if (e != hipSuccess) return e;
+        }
+        chain = g_rec_chain[dev];
+        e = hipStreamWaitEvent(s, chain, 0);  // (an event never recorded: no wait)
+        if (e != hipSuccess) return e;
+      }
+    }
     hipLaunchKernelGGL(kern, grid, block, 0, s, Whh_f, Gin, xin, out, x16, hx, hfin, cst, lens, B, Bp, Tp, residual,
                        err, trace, nrg, sleep, gap, plain, km);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && chain) e = hipEventRecord(chain, s);
+    return e;
   };
   switch (layout) {
     case 1: return s16 ? go(rec_layer_kernel<16, 32, true>) : go(rec_layer_kernel<16, 32, false>);

@@ -235,10 +235,14 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *   CASR_OPT_REC_SLEEP       pacing of the recurrence's first poll per step, x 64 clocks (default 1)
  *   CASR_OPT_REC_POLL_GAP    second poll of a pass issued this many x 64 clocks after the first
  *                            (1..8, default 2)
- *   CASR_OPT_REC_COOP        1: the persistent recurrence is a cooperative launch, so a grid that
- *                            cannot be co-resident fails at launch (the encode then falls back to
- *                            the per-step recurrence) instead of spinning into the hand-off timeout;
- *                            0: ordinary launch after the occupancy check
+ *   CASR_OPT_REC_COOP        2 (default, round 6): the persistent recurrence is an ordinary launch
+ *                            after the occupancy check, ordered after the previous persistent launch
+ *                            of this process on the same device (a process-wide event per device), so
+ *                            two persistent grids of batches in flight never share the chip; 1: a
+ *                            cooperative launch, so a grid that cannot be co-resident fails at launch
+ *                            (the encode then falls back to the per-step recurrence) instead of
+ *                            spinning into the hand-off timeout (about 25 us more per launch);
+ *                            0: ordinary launch, unordered
  *   CASR_OPT_GEMM16_PERSIST  s16x3 input-projection kernel: 2 persistent ping-pong form (default: two
  *                            wave groups one barrier apart, 16-deep stages on a ring of four); 1
  *                            persistent, 32-deep stages on two buffers; 0 one workgroup per tile

@@ -324,8 +324,8 @@ def test_beam_select_in_attention_equals_select_launches(eng, k, eos_bias, graph
 
 @pytest.mark.parametrize("B,layout", [(37, 0), (37, 1), (37, 2), (256, 0)])
 def test_persistent_recurrence_equals_per_step(eng, B, layout):
-    """The persistent per-layer recurrence (granule hand-offs, either store flavour, ordinary or
-    cooperative launch) and the per-step launches give bitwise-identical encoder outputs and
+    """The persistent per-layer recurrence (granule hand-offs, either store flavour; chained
+    ordinary, cooperative or unordered launch) and the per-step launches give bitwise-identical encoder outputs and
     final states, on ragged lengths (B = 37: a partial row group and padding rows, in the 16x16
     layout the batch selects and in the forced 32x16 and 16x32 ones; B = 256: the full
     256-workgroup grid of 32x16)."""
@@ -342,11 +342,11 @@ def test_persistent_recurrence_equals_per_step(eng, B, layout):
                               torch.from_numpy(frames.astype(np.int32)).to(eng.device))
     assert eng.recurrence_mode(B) == 1, "B <= 256 must take the persistent path on MI355X"
     outs = []
-    # the persistent path three times: hand-off words stored plain (L2-kept, the default when each
-    # group shares an XCD) and write-through (CASR_OPT_REC_STORE_PLAIN = 0), cooperative launch
-    # (default) and ordinary launch (CASR_OPT_REC_COOP = 0)
+    # the persistent path four times: hand-off words stored plain (L2-kept, the default when each
+    # group shares an XCD) and write-through (CASR_OPT_REC_STORE_PLAIN = 0), the chained ordinary
+    # launch (default, CASR_OPT_REC_COOP = 2), the cooperative launch (1) and the unordered one (0)
     try:
-        for persistent, plain, coop in ((False, 1, 1), (True, 1, 1), (True, 0, 1), (True, 1, 0)):
+        for persistent, plain, coop in ((False, 1, 2), (True, 1, 2), (True, 0, 2), (True, 1, 1), (True, 1, 0)):
             eng.set_option("REC_STORE_PLAIN", plain)
             eng.set_option("REC_COOP", coop)
             eng.set_persistent(persistent)
@@ -354,7 +354,7 @@ def test_persistent_recurrence_equals_per_step(eng, B, layout):
             assert eng.device_flags() == 0
             outs.append([t.cpu() for t in eng.encoder_results()])
     finally:
-        for k, v in (("REC_STORE_PLAIN", 1), ("REC_COOP", 1), ("REC_LAYOUT", 0)):
+        for k, v in (("REC_STORE_PLAIN", 1), ("REC_COOP", 2), ("REC_LAYOUT", 0)):
             eng.set_option(k, v)
         eng.set_persistent(True)
     for got in outs[1:]:

@@ -16,13 +16,14 @@
 #   pmc              PMC passes of tools/probes/one_step.py (PMC_MODES: greedy and/or beam) with the
 #                    counter sets in PMC_SETS (';'-separated passes) into $OUT/pmc<PMC_TAG>_<mode>;
 #                    CASR_OPTS=$PMC_OPTS (default REC_COOP=0, the ordinary recurrence launch: DESIGN
-#                    3.2, a cooperative launch ends in SIGSEGV under rocprofv3)
+#                    3.2, a cooperative launch (REC_COOP=1) ends in SIGSEGV under rocprofv3)
 #   profbeam         rocprofv3 kernel trace + stats of tools/probes/one_step.py at beam 8, B = 256 and 128
 #   probe            python $PROBE once (tools/probes/*.py)
 #   ablibs           tools/probes/ab_libs.sh (LIBS, AB_ARGS, AB_ROUNDS): interleaved library-build A/B
 #   trace            tools/rec_trace.py
 #   prof             rocprofv3 kernel trace + stats of bench.py (greedy only) on the shipped
-#                    cooperative launch; its exit status is recorded (must be the LAST stage)
+#                    recurrence launch (round 6: chained ordinary, REC_COOP=2); its exit status is
+#                    recorded (must be the LAST stage)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/session}
@@ -111,7 +112,7 @@ for s in $STAGES; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
         python3 bench.py --steps 20 --warmup 2 --streams 1 --no-beam --no-configs --no-f32-compare --no-cpu-baseline \
         > $OUT/prof_bench.json 2> $OUT/prof.err
-      echo "rocprofv3 kernel trace of the default (cooperative) launch: exit status $?" | tee $OUT/prof_rc.txt
+      echo "rocprofv3 kernel trace of the default recurrence launch: exit status $?" | tee $OUT/prof_rc.txt
       python tools/prof_by_grid.py $OUT/prof/run_kernel_trace.csv 30 > $OUT/prof_by_grid.txt 2>&1
       head -14 $OUT/prof_by_grid.txt
       break ;;
