@@ -354,13 +354,17 @@ def main():
     step_greedy()
     breakdown = eng.profile_read()
     dominant = max(breakdown, key=lambda c: breakdown[c][1])
-    # Two timed regions of the same steps.  (1) Serial, one batch in flight: the dominant class keeps
-    # its event pair per launch, so `roofline` is the kernel's own launch duration (as rocprof sees it
-    # in a serial run).  (2) args.streams batches in flight (casr.pipeline): the line's `value`, the
-    # whole-job throughput; a launch there shares the chip with the other batch's kernels, so its span
-    # is longer (reported as roofline.pipelined_avg_launch_us) while the chip does more work per second.
-    pipe.profile([dominant])
+    # Timed regions of the same steps.  (1) Serial, one batch in flight: `greedy_serial`, the
+    # latency.  (2) The same with the dominant class's event pair around each of its launches, so
+    # `roofline` is the kernel's own launch duration (as rocprof sees it in a serial run); the event
+    # records cost the step a few microseconds per launch (an event timestamp waits for the previous
+    # kernel), so this pass times nothing else.  (3) args.streams batches in flight (casr.pipeline),
+    # uninstrumented: the line's `value`, the whole-job throughput.  (4) The same with the dominant
+    # class's events: a launch there shares the chip with the other batch's kernels, so its span is
+    # longer (roofline.pipelined_avg_launch_us) while the chip does more work per second.
     dt_serial = timed(step_greedy, args.steps, "greedy_serial", n=1)
+    pipe.profile([dominant])
+    dt_serial_prof = timed(step_greedy, args.steps, "greedy_serial_profiled", n=1)
     dom_launches, dom_ms = pipe.profile_read()[dominant]
     pipe.profile([])
     pl_dom = None
@@ -368,8 +372,9 @@ def main():
         for _ in range(args.streams):  # every handle of the timed region warm
             pipe.submit(step_greedy, args.streams)
         flags["warmup_pipeline"] = pipe.device_flags()
-        pipe.profile([dominant])
         dt = timed(step_greedy, args.steps, "greedy", n=args.streams)
+        pipe.profile([dominant])
+        timed(step_greedy, args.steps, "greedy_pipelined_profiled", n=args.streams)
         pl_dom = pipe.profile_read()[dominant]
         pipe.profile([])
     else:
@@ -699,7 +704,10 @@ def main():
             "greedy_serial": {"value": B * world * args.steps / dt_serial, "unit": "utt/s",
                               "ms_per_step": 1000.0 * dt_serial / args.steps,
                               "device_ms_per_step": step_stats("greedy_serial"),
-                              "note": "the same steps with one batch in flight (the round-5 headline's loop)"},
+                              "ms_per_step_with_dominant_events": 1000.0 * dt_serial_prof / args.steps,
+                              "note": "the same steps with one batch in flight (the round-5 headline's loop); "
+                                      "ms_per_step_with_dominant_events: the roofline's pass, an event pair "
+                                      "around each launch of the dominant class"},
             "device_ms_per_step": step_stats("greedy"),
             "device_ms_note": "per timed step, HIP events on the compute stream around each step (device "
                               "time incl. any launch gaps; SURVEY 8d: median of the steps)",
@@ -713,8 +721,9 @@ def main():
                          "traffic_unit": "bytes per launch (PMC 2 x FETCH_SIZE + WRITE_SIZE)",
                          "algorithmic_bytes": kernel_bytes(dominant, B, Tp, B, cfg.vocab, fold, precision == "s16x3"),
                          "launches": dom_launches, "avg_launch_us": 1e6 * avg_launch_s,
-                         "timed_region": "serial pass (one batch in flight) of the same greedy steps; the headline "
-                                         "value is the pass with `batches_in_flight` batches in flight",
+                         "timed_region": "serial pass (one batch in flight) of the same greedy steps with this "
+                                         "class's event pairs; the headline value is the uninstrumented pass with "
+                                         "`batches_in_flight` batches in flight",
                          "pipelined_avg_launch_us": pl_roof["avg_launch_us"] if pl_roof else None,
                          "pipelined_frac": pl_roof["frac"] if pl_roof else None,
                          "launch": LAUNCH_UNIT.get(dominant, "one kernel launch"),
