@@ -191,8 +191,8 @@ def relaunch(n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--frames", type=int, default=800)
     ap.add_argument("--beam", type=int, default=8)
@@ -354,19 +354,19 @@ def main():
     step_greedy()
     breakdown = eng.profile_read()
     dominant = max(breakdown, key=lambda c: breakdown[c][1])
-    # Timed regions of the same steps.  (1) Serial, one batch in flight: `greedy_serial`, the
-    # latency.  (2) The same with the dominant class's event pair around each of its launches, so
-    # `roofline` is the kernel's own launch duration (as rocprof sees it in a serial run); the event
-    # records cost the step a few microseconds per launch (an event timestamp waits for the previous
-    # kernel), so this pass times nothing else.  (3) args.streams batches in flight (casr.pipeline),
+    # Timed regions of the same steps.  (1) Serial, one batch in flight, with the dominant class's
+    # event pair around each of its launches, so `roofline` is the kernel's own launch duration (as
+    # rocprof sees it in a serial run); the event records cost the step a few microseconds per launch
+    # (an event timestamp waits for the previous kernel), so this pass times nothing else.  (2) The
+    # same uninstrumented: `greedy_serial`, the latency.  (3) args.streams batches in flight (casr.pipeline),
     # uninstrumented: the line's `value`, the whole-job throughput.  (4) The same with the dominant
     # class's events: a launch there shares the chip with the other batch's kernels, so its span is
     # longer (roofline.pipelined_avg_launch_us) while the chip does more work per second.
-    dt_serial = timed(step_greedy, args.steps, "greedy_serial", n=1)
     pipe.profile([dominant])
     dt_serial_prof = timed(step_greedy, args.steps, "greedy_serial_profiled", n=1)
     dom_launches, dom_ms = pipe.profile_read()[dominant]
     pipe.profile([])
+    dt_serial = timed(step_greedy, args.steps, "greedy_serial", n=1)
     pl_dom = None
     if args.streams > 1:
         for _ in range(args.streams):  # every handle of the timed region warm
