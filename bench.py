@@ -207,7 +207,7 @@ def main():
                          "config 5 (beam 16 + LM) side lines")
     ap.add_argument("--sharded-batch", type=int, default=1024,
                     help="global batch of the BASELINE config 4 / 5 lines (partitioned over the ranks)")
-    ap.add_argument("--rescore-workers", type=int, default=6,
+    ap.add_argument("--rescore-workers", type=int, default=12,
                     help="host worker processes per rank for config 5's second-pass LM calls (0: in-process)")
     ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--cpu-beam-sample", type=int, default=64)
