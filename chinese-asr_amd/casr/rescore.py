@@ -69,27 +69,31 @@ class ParallelRescorer:
             # ids outside int2word: the in-process form (its own fallback) decides
             return second_pass_arrays(rec_tokens, rec_score, rec_valid, dict(enumerate(self.words)),
                                       self.lm_factory(), lm_weight, length_weight)
-        scores = rec_score[bs, ls, cs].tolist()
-        lens = ls.tolist()
-        starts = np.flatnonzero(np.r_[True, bs[1:] != bs[:-1]]).tolist() + [len(bs)]
-        multi = [(a, z) for a, z in zip(starts[:-1], starts[1:]) if z - a > 1]
+        n = len(bs)
+        sc32 = rec_score[bs, ls, cs]
+        starts = np.flatnonzero(np.r_[True, bs[1:] != bs[:-1]])
+        size = np.diff(np.r_[starts, n])
         # the records whose sentences the LM scores (every record of a multi-record utterance), in order
-        idx = np.concatenate([np.arange(a, z) for a, z in multi]) if multi else np.zeros(0, np.int64)
-        lm = np.empty(len(bs), np.float64)
+        multi = np.repeat(size > 1, size)
+        idx = np.flatnonzero(multi)
+        lm = np.zeros(n, np.float64)
         if len(idx):
             t16 = full[idx].astype(np.int16)
             l32 = ls[idx].astype(np.int32)
             tasks = [(t16[i:i + self.chunk], l32[i:i + self.chunk]) for i in range(0, len(idx), self.chunk)]
             out = self.pool.map(_score, tasks)
             lm[idx] = [q for part in out for q in part]
-        res = {}
-        for a, z in zip(starts[:-1], starts[1:]):
-            b = int(bs[a])
-            if z - a == 1:
-                res[b] = (full[a, :lens[a]].tolist(), scores[a])
-                continue
-            comb = [sc + lm_weight * float(q) + length_weight * l
-                    for sc, q, l in zip(scores[a:z], lm[a:z].tolist(), lens[a:z])]
-            i = a + int(np.argmax(comb))
-            res[b] = (full[i, :lens[i]].tolist(), scores[i])
-        return res
+        # comb = logp + lm_w * LM + len_w * len per record, as second_pass_arrays evaluates it on Python
+        # floats: (logp + (lm_w * q)) + (len_w * l), each an IEEE double operation, so the vector form
+        # gives the same bits; then the first maximum per utterance (np.argmax's choice)
+        comb = (sc32.astype(np.float64) + lm_weight * lm) + length_weight * ls.astype(np.float64)
+        seg_max = np.maximum.reduceat(comb, starts)
+        pos = np.where(comb == np.repeat(seg_max, size), np.arange(n), n)
+        first = np.minimum.reduceat(pos, starts)
+        for j in np.flatnonzero(first >= n):  # a NaN in the utterance: np.argmax's first-NaN rule
+            first[j] = starts[j] + int(np.argmax(comb[starts[j]:starts[j] + size[j]]))
+        first = np.where(size == 1, starts, first)  # one record: it (no LM call, model.py:749-763)
+        scores = sc32[first].tolist()
+        lens = ls[first].tolist()
+        rows = full[first]
+        return {int(bs[i]): (rows[j, :lens[j]].tolist(), scores[j]) for j, i in enumerate(first.tolist())}

@@ -106,6 +106,30 @@ def test_parallel_rescorer_equals_second_pass_arrays():
                 rt[b, l, c, :l] = rs_.randint(0, 5004, size=l)
             rsc = rs_.randn(B, L, k).astype(np.float32)
             assert pr.select(rt, rsc, rv, 1.5, 1.5) == second_pass_arrays(rt, rsc, rv, i2w, StubLM(), 1.5, 1.5)
+        # exact ties (identical records: the first one wins), -inf and NaN scores (np.argmax takes the
+        # first NaN), an utterance with one record (no LM call)
+        B, L, k = 5, 10, 4
+        rv = np.zeros((B, L, k), np.uint8)
+        rt = np.full((B, L, k, L), -1, np.int32)
+        rsc = rs_.randn(B, L, k).astype(np.float32)
+        for b in range(4):
+            for l, c in ((3, 0), (3, 1), (5, 2), (7, 3)):
+                rv[b, l, c] = 1
+                rt[b, l, c, :l] = (np.arange(l) * 7 + b) % 5004
+        rt[0, 3, 1] = rt[0, 3, 0]
+        rsc[0, 3, 1] = rsc[0, 3, 0]          # utterance 0: a tie between its first two records
+        rsc[0, 5, 2] = rsc[0, 7, 3] = -50.0
+        rsc[1, 5, 2] = -np.inf               # utterance 1: -inf in one record
+        rsc[2, 5, 2] = np.nan                # utterance 2: a NaN record
+        rv[4, 6, 1] = 1
+        rt[4, 6, 1, :6] = 11                 # utterance 4: one record
+        got = pr.select(rt, rsc, rv, 1.5, 1.5)
+        want = second_pass_arrays(rt, rsc, rv, i2w, StubLM(), 1.5, 1.5)
+        assert got.keys() == want.keys()
+        for b in want:
+            assert got[b][0] == want[b][0], b
+            assert got[b][1] == want[b][1] or (np.isnan(got[b][1]) and np.isnan(want[b][1])), b
+        assert np.isnan(got[2][1]) and got[0][0] == rt[0, 3, 0, :3].tolist()
     finally:
         pr.close()
 
