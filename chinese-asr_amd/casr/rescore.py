@@ -80,7 +80,9 @@ class ParallelRescorer:
         if len(idx):
             t16 = full[idx].astype(np.int16)
             l32 = ls[idx].astype(np.int32)
-            tasks = [(t16[i:i + self.chunk], l32[i:i + self.chunk]) for i in range(0, len(idx), self.chunk)]
+            # about two tasks per worker (every worker busy, the last ones short), at most self.chunk rows
+            step = max(64, min(self.chunk, -(-len(idx) // (2 * self.workers))))
+            tasks = [(t16[i:i + step], l32[i:i + step]) for i in range(0, len(idx), step)]
             out = self.pool.map(_score, tasks)
             lm[idx] = [q for part in out for q in part]
         # comb = logp + lm_w * LM + len_w * len per record, as second_pass_arrays evaluates it on Python
