@@ -91,3 +91,30 @@ def test_shard_decoder_over_pipeline_equals_engine():
     finally:
         pipe.close()
     np.testing.assert_array_equal(got, want)
+
+
+def test_full_chip_encoders_on_four_streams():
+    """Four B = 256 encodes in flight on four handles / streams: every persistent layer wants all 256
+    CUs, and its workgroups wait on each other, so two of them placed side by side could each hold
+    part of the chip and wait forever (until the 2 s hand-off bound).  The library orders the
+    persistent launches of a process per device (CASR_OPT_REC_COOP = 2, recurrence.hip): no guard
+    bit, and every handle's encoder results equal the serial ones, over two rounds."""
+    from casr.pipeline import StreamPipeline
+    blob = torch.from_numpy(pack_weights(CFG, *synthetic_state_dicts(CFG, peaked=True))).cuda()
+    fb, fr = _batch(256, 800, 11)
+    torch.cuda.synchronize()
+    pipe = StreamPipeline(CFG, blob, n=4)
+    try:
+        assert all(e.get_option("REC_COOP") == 2 for e in pipe.engines)
+        e0 = pipe.engines[0]
+        e0.encode_fbank(fb, fr)
+        want = [t.cpu() for t in e0.encoder_results()]
+        for _ in range(2):
+            outs = [pipe.submit(lambda e: (e.encode_fbank(fb, fr), e.encoder_results())[1]) for _ in range(4)]
+            torch.cuda.synchronize()
+            assert pipe.device_flags() == 0
+            for got in outs:
+                for a, b in zip(want, got):
+                    assert torch.equal(a, b.cpu())
+    finally:
+        pipe.close()
