@@ -77,7 +77,7 @@ Layout make_layout(const casr_config& cfg);
 // Tuning options of a handle (include/casr.h CASR_OPT_*): speed only, every value gives the same
 // bits (CASR_OPT_ATTN_DIRECT: a numerics variant within the attention tolerance).
 struct Tuning {
-  int v[CASR_OPT_COUNT] = {1, 0, 1, 0, 2, 2, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1, 1, 0, 0};
+  int v[CASR_OPT_COUNT] = {1, 0, 1, -1, 2, 2, 2, 2, 0, 0, 1, 0, 0, 1, 1, 1, 1, 0, 0};
   int operator[](int i) const { return v[i]; }
 };
 

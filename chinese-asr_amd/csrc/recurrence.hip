@@ -496,7 +496,10 @@ hipError_t launch_rec_layer(const float* Whh_f, const float* Gin, const float* x
   int Bp = (B + 31) / 32 * 32;  // granule planes padded to 32 rows for every layout
   const int RG = rec_rows(layout), UW = rec_units(layout);
   int nrg = (B + RG - 1) / RG;
-  int sleep = t[CASR_OPT_REC_SLEEP] < 0 ? 0 : t[CASR_OPT_REC_SLEEP] > 16 ? 16 : t[CASR_OPT_REC_SLEEP];
+  // (-1, the default: no sleep for grids of 64 workgroups or more, one unit below: B <= 16 in the
+  // 16-row layout, 32 workgroups; measured round 6)
+  const int nwg = (H / UW) * nrg * 2;
+  int sleep = t[CASR_OPT_REC_SLEEP] < 0 ? (nwg >= 64 ? 0 : 1) : t[CASR_OPT_REC_SLEEP] > 16 ? 16 : t[CASR_OPT_REC_SLEEP];
   int gap = t[CASR_OPT_REC_POLL_GAP] < 1 ? 1 : t[CASR_OPT_REC_POLL_GAP] > 8 ? 8 : t[CASR_OPT_REC_POLL_GAP];
   int plain = t[CASR_OPT_REC_STORE_PLAIN] ? 1 : 0;
   const dim3 grid((H / UW) * nrg * 2), block(RG * UW);

@@ -232,8 +232,10 @@ int casr_recurrence_mode(const casr_handle* h, int B);
  *                            2 16x32, 3 16x16
  *   CASR_OPT_REC_STORE_PLAIN 1: hand-off words stored L2-kept when the workgroup's whole hand-off
  *                            group runs on its XCD (checked per launch; default); 0: write-through
- *   CASR_OPT_REC_SLEEP       pacing of the recurrence's first poll per step, x 64 clocks (default 0
- *                            since round 6: 1 measured 2-3 % slower in the 16-row layouts, B <= 128)
+ *   CASR_OPT_REC_SLEEP       pacing of the recurrence's first poll per step, x 64 clocks; -1
+ *                            (default, round 6): 0 for grids of 64 workgroups or more, 1 below
+ *                            (B <= 16); measured: 0 is 2-3 % faster at B = 32 and 128, 1 is 1.6 %
+ *                            faster at B = 1
  *   CASR_OPT_REC_POLL_GAP    second poll of a pass issued this many x 64 clocks after the first
  *                            (1..8, default 2)
  *   CASR_OPT_REC_COOP        2 (default, round 6): the persistent recurrence is an ordinary launch

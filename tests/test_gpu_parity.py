@@ -414,14 +414,14 @@ def test_recurrence_pacing_options_bitwise(eng):
     feat, flen = _bench_batch(eng, 256)
     outs = []
     try:
-        for sleep, gap in ((0, 2), (1, 2), (0, 1), (16, 8), (4, 1)):
+        for sleep, gap in ((-1, 2), (1, 2), (0, 1), (16, 8), (4, 1)):
             eng.set_option("REC_SLEEP", sleep)
             eng.set_option("REC_POLL_GAP", gap)
             eng.encode(feat, flen)
             assert eng.device_flags() == 0
             outs.append([t.cpu() for t in eng.encoder_results()])
     finally:
-        eng.set_option("REC_SLEEP", 0)
+        eng.set_option("REC_SLEEP", -1)
         eng.set_option("REC_POLL_GAP", 2)
     for got in outs[1:]:
         for a, b in zip(outs[0], got):
